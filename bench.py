@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py — throughput of the MI355X smallpt sampling loop (BASELINE.json metric: Msamples/s).
+
+A "step" = one render of the workload through the C ABI (spt_render_async: scene upload, queue
+reset, render kernel, fixed-point -> float finalize) into a device framebuffer, plus (N > 1) the
+single RCCL gather of the fp32 row tiles to rank 0. Inputs (scene, camera) are built once; the
+framebuffers stay resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--no-cpu-baseline]
+  torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU, RCCL)
+
+Workloads (BASELINE.json configs):
+  c2  1024x768 @ 64 spp, cosine-weighted (:474-477)
+  c3  1024x768 @ 512 spp, explicit light sampling (:464-473)   <- default, the north-star config
+  c4  4096x4096 @ 1024 spp, NEE                                 (8-GPU config; strong by default)
+  c5  4096x4096 @ 4096 spp, 32-sphere scene, max depth 16       (8-GPU config; strong by default)
+Weak scaling (default for c2/c3): each of N GPUs renders 1/N of the rows at N x spp, so per-GPU
+work is the single-GPU workload and the N-GPU job is the same image at N x the samples.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec (w×h×spp/s) on Cornell box; per-channel RMSE vs ref PPM"
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (v_fma_f32 on all lanes)
+CONFIGS = {
+    "c2": dict(width=1024, height=768, spp=64, nee_prob=0.0, scene="cornell", max_depth=0,
+               scaling="weak", desc="C2: 1024x768 @ 64 spp, cosine-weighted importance sampling"),
+    "c3": dict(width=1024, height=768, spp=512, nee_prob=1.0, scene="cornell", max_depth=0,
+               scaling="weak", desc="C3: 1024x768 @ 512 spp, Cornell box + explicit light sampling"),
+    "c4": dict(width=4096, height=4096, spp=1024, nee_prob=1.0, scene="cornell", max_depth=0,
+               scaling="strong", desc="C4: 4096x4096 @ 1024 spp, NEE, row-tile shards"),
+    "c5": dict(width=4096, height=4096, spp=4096, nee_prob=1.0, scene="spheres32", max_depth=16,
+               scaling="strong", desc="C5: 4096x4096 @ 4096 spp, 32-sphere scene, max depth 16"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
+    """Counter-mode oracle (the same algorithm and random stream as the kernel) on the host cores,
+    OpenMP over a cyclic row subset, sized to ~budget_s; also checks those rows bit-exactly."""
+    from oracle import oracle
+
+    threads = min(16, os.cpu_count() or 1)
+    h, w, spp = params.height, params.width, params.spp
+    t0 = time.perf_counter()
+    oracle.counter_render(prims, cam._c, params, rows=np.array([h // 2], np.int32), threads=threads)
+    t_row = max(time.perf_counter() - t0, 1e-3)
+    n_rows = int(max(1, min(h, round(budget_s / t_row))))
+    stride = max(1, h // n_rows)
+    rows = np.arange(stride // 2, h, stride, dtype=np.int32)[:n_rows]
+    t0 = time.perf_counter()
+    img, st = oracle.counter_render(prims, cam._c, params, rows=rows, threads=threads)
+    dt = time.perf_counter() - t0
+    samples = len(rows) * w * spp
+    exact = gpu_img is not None and np.array_equal(gpu_img[rows], img)
+    return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{len(rows)} of {h} rows (every {stride}th), {w}x{spp} spp each = "
+                      f"{samples} samples in {dt:.1f} s; oracle/spt_oracle.c counter mode, "
+                      f"OpenMP dynamic rows",
+            "gpu_rows_bit_exact": bool(exact)}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
+    ap.add_argument("--spp", type=int, default=0, help="override spp (per-GPU for weak scaling)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
+                    help="PMC traffic summary (HBM bytes per render launch) to attach, if present")
+    ap.add_argument("--save-ppm", default="")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    spt = importlib.import_module("small-pathtracer_amd")
+    cfg = dict(CONFIGS[args.config])
+    scaling = args.scaling or cfg["scaling"]
+    spp = args.spp or cfg["spp"]
+    if scaling == "weak":
+        spp *= world
+    prims = spt.cornell_scene() if cfg["scene"] == "cornell" else spt.spheres32_scene()
+    w, h = cfg["width"], cfg["height"]
+    cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    params = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
+                                max_depth=cfg["max_depth"], tile_rows=8, shard_index=rank,
+                                shard_count=world, device=local)
+    rows_of = [spt.shard_rows(spt.default_params(height=h, tile_rows=8, shard_index=k,
+                                                 shard_count=world)) for k in range(world)]
+    my_rows = rows_of[rank]
+    max_rows = max(len(r) for r in rows_of)
+
+    ren = spt.Renderer(local)
+    ren.reserve(len(prims), params)
+    stream = torch.cuda.current_stream()
+    shard = torch.zeros((max_rows, w, 3), dtype=torch.float32, device="cuda")
+    full = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
+    gather_list = ([torch.empty_like(shard) for _ in range(world)] if (rank == 0 and world > 1)
+                   else None)
+    row_idx = [torch.as_tensor(r, dtype=torch.long, device="cuda") for r in rows_of]
+    kstats = []
+
+    def step():
+        ren.render_async(prims, cam, params, shard.data_ptr(), stream.cuda_stream)
+        kstats.append(ren.stats())
+        if world > 1:
+            dist.gather(shard, gather_list, dst=0)
+            if rank == 0:
+                for k in range(world):
+                    full.index_copy_(0, row_idx[k], gather_list[k][: len(rows_of[k])])
+        else:
+            full.copy_(shard[: len(my_rows)])
+
+    for _ in range(args.warmup):
+        step()
+    kstats.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = w * h * spp  # all ranks together (each rank renders its rows at spp)
+    value = samples_per_step * args.steps / elapsed / 1e6
+    kms = np.array([s["kernel_ms"] for s in kstats])
+    flop = np.array([s["flop"] for s in kstats])
+    achieved = float((flop / (kms * 1e-3)).mean() / 1e12)
+    s0 = kstats[-1]
+    my_samples = len(my_rows) * w * spp
+    assert s0["samples"] == my_samples, (s0["samples"], my_samples)
+
+    traffic = None
+    if os.path.exists(args.traffic) and args.config == "c3" and world == 1:
+        try:
+            traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    if rank == 0:
+        img = full.cpu().numpy()
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
+        if args.save_ppm:
+            spt.write_ppm(args.save_ppm, img)
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: the reference's Cornell-box scene (smallpt.cpp:287-311) and camera "
+                    "(:521), Philox4x32-10 stream seed 1",
+            "config": {"workload": cfg["desc"] + (f", weak-scaled to {spp} spp over {world} GPUs"
+                                                   if scaling == "weak" and world > 1 else ""),
+                       "width": w, "height": h, "spp": spp,
+                       "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",
+                       "parallelism": f"row-tile x{world} (tile 8 rows, cyclic) + RCCL gather"
+                                      if world > 1 else "1 GPU"},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": traffic, "kernel": "spt::render_kernel",
+                         "kernel_ms": round(float(kms.mean()), 3),
+                         "flop_per_launch": float(flop.mean()),
+                         "flop_per_sample": round(float(flop.mean()) / my_samples, 1)},
+            "paths": {"vertices_per_sample": round(s0["vertices"] / my_samples, 4),
+                      "rays_per_sample": round((s0["path_rays"] + s0["shadow_rays"]) / my_samples, 4),
+                      "misses_per_sample": round(s0["misses"] / my_samples, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ren.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

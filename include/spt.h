@@ -1,0 +1,154 @@
+/*
+ * spt.h — C ABI of the MI355X-native smallpt sampling loop (small-pathtracer_amd).
+ *
+ * Drop-in boundary for the reference's per-pixel sampling loop
+ *   /root/reference/src/smallpt.cpp:528-542  (main: row/col/sample loops, r += radiance()/spp, c[i] = clamp(r))
+ * whose per-sample kernel is radiance() at :419-496 (live path tracer :444-480).
+ * The reference has no plugin/operator/FFI API; its de-facto inputs are globals and locals:
+ *   scene  Hitable *rect[NUMBER_OBJ]         :287-311   -> spt_prim[] (tagged flat records)
+ *   camera Camera cam(LOOKFROM, ...)         :262-279, :521 -> spt_camera
+ *   w, h, samps                              :507-508   -> spt_params.width/height/spp
+ *   srand(time) / Xi={0,0,y^3}               :503, :530 -> spt_params.seed (counter-based Philox stream)
+ * and its output is Vec *c (w*h RGB, clamped to [0,1], row-major, y=0 = top row) :510, :538,
+ * consumed by the PPM writer :548-551 -> rgb_out (float, same layout/clamping).
+ *
+ * Conventions: extern "C", plain pointers and sizes, no exceptions cross the ABI, every entry
+ * point returns an spt_status. Buffers are caller-owned. One spt_context per HIP device; calls on
+ * different contexts may run concurrently, calls on one context must be serialised by the caller.
+ */
+#ifndef SPT_H_
+#define SPT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPT_ABI_VERSION 1
+
+typedef enum spt_status {
+  SPT_OK = 0,
+  SPT_ERR_INVALID_ARG = 1, /* bad sizes, null pointers, unsupported scene/params */
+  SPT_ERR_HIP = 2,         /* a HIP runtime call failed (spt_last_error() has the text) */
+  SPT_ERR_NO_DEVICE = 3,   /* no usable gfx950 device */
+  SPT_ERR_OOM = 4,         /* device allocation failed */
+  SPT_ERR_UNSUPPORTED = 5  /* feature not implemented (e.g. SPEC/REFR material) */
+} spt_status;
+
+/* Primitive kinds: the reference's Hitable subclasses (:92-254). */
+typedef enum spt_kind {
+  SPT_RECT_XY = 0, /* Rectangle_xy(x1,x2,y1,y2,z, e,c,refl)  :137-178, plane z=k  */
+  SPT_RECT_XZ = 1, /* Rectangle_xz(x1,x2,z1,z2,y, e,c,refl)  :92-135,  plane y=k  */
+  SPT_RECT_YZ = 2, /* Rectangle_yz(y1,y2,z1,z2,x, e,c,refl)  :180-221, plane x=k  */
+  SPT_SPHERE = 3   /* Sphere(rad, p, e, c, refl)             :223-254             */
+} spt_kind;
+
+/* Refl_t :72-74. Only DIFF is live in the reference (:457); SPEC/REFR are commented out (:481-495). */
+typedef enum spt_refl { SPT_DIFF = 0, SPT_SPEC = 1, SPT_REFR = 2 } spt_refl;
+
+/* One scene primitive. geom[] holds the constructor arguments in the reference's order:
+ *   RECT_XY: {x1, x2, y1, y2, z}   RECT_XZ: {x1, x2, z1, z2, y}   RECT_YZ: {y1, y2, z1, z2, x}
+ *   SPHERE : {rad, px, py, pz, 0}
+ * e = emission, c = colour (Vec e, c in the reference). Doubles mirror the reference constructors;
+ * the device path rounds them to fp32 once per render. */
+typedef struct spt_prim {
+  int32_t kind;  /* spt_kind */
+  int32_t refl;  /* spt_refl */
+  double geom[5];
+  double e[3];
+  double c[3];
+} spt_prim;
+
+/* Camera :256-285 — the four vectors its constructor computes (:267-274). Build with
+ * spt_camera_init() for the reference's constructor semantics (float vfov/aspect, tanf). */
+typedef struct spt_camera {
+  double origin[3];
+  double lower_left_corner[3];
+  double horizontal[3];
+  double vertical[3];
+} spt_camera;
+
+/* Light-sample arithmetic of light_sampling() :363-369:  x = 32 + rand()*36/double(RAND_MAX).
+ * With glibc (RAND_MAX = 2^31-1) rand()*36 overflows int32 and wraps, so the reference as built
+ * on Linux samples x in [31,33], z in [62,64] (measured). GLIBC_WRAP reproduces that arithmetic
+ * on a 31-bit draw; UNIFORM is the intended [x0, x0+dx] x [z0, z0+dz] (MinGW RAND_MAX=32767). */
+typedef enum spt_light_mode { SPT_LIGHT_GLIBC_WRAP = 0, SPT_LIGHT_UNIFORM = 1 } spt_light_mode;
+
+typedef struct spt_params {
+  int32_t width, height, spp; /* :507-508 */
+  uint32_t seed;              /* Philox4x32-10 key word 0 (key word 1 = SPT_PHILOX_KEY1) */
+  float nee_prob;             /* Q of :464 (`q < Q`): 1 = HEAD explicit light sampling, 0 = cosine only */
+  int32_t rr_depth;           /* Russian roulette starts when ++depth > rr_depth  (:448, HEAD = 5) */
+  int32_t max_depth;          /* 0 = unbounded (reference); >0 = path ends at this vertex depth */
+  int32_t light_id;           /* primitive index treated as "the light" by NEE (:467, HEAD = 6) */
+  float light_x0, light_dx;   /* light sample rect x0 + [0,dx] (:365)   HEAD 32, 36 */
+  float light_z0, light_dz;   /* light sample rect z0 + [0,dz] (:366)   HEAD 63, 36 */
+  float light_y;              /* sample plane y (:367)                  HEAD 81.6   */
+  float light_area;           /* PDF area constant (:471)               HEAD 1296   */
+  int32_t light_mode;         /* spt_light_mode */
+  /* Row sharding (multi-GPU): tiles of tile_rows image rows, tile t rendered by shard t % shard_count.
+   * The output of a shard holds only its rows, compacted in increasing row order (spt_shard_rows). */
+  int32_t tile_rows;          /* 0 -> 8 */
+  int32_t shard_index, shard_count;
+  int32_t chunk;              /* samples per work unit (0 = auto). Never changes results. */
+  int32_t device;             /* HIP device ordinal for spt_render() */
+  uint32_t flags;             /* reserved, must be 0 */
+} spt_params;
+
+#define SPT_PHILOX_KEY1 0x53505431u /* "SPT1" */
+
+/* Per-render path statistics (counted in-kernel, summed once per wave). */
+typedef struct spt_stats {
+  uint64_t samples;        /* pixel-samples finished = camera rays */
+  uint64_t path_rays;      /* rays traced through the scene for path vertices (incl. camera rays) */
+  uint64_t shadow_rays;    /* NEE shadow rays traced */
+  uint64_t vertices;       /* path vertices shaded (incl. terminal ones) */
+  uint64_t nee_events;     /* NEE light samples taken (:465) */
+  uint64_t nee_light_hits; /* ... whose shadow ray hit light_id (:470-472) */
+  uint64_t cosine_samples; /* cosine-weighted scatter directions drawn (:337-347) */
+  uint64_t misses;         /* path rays that hit nothing (reference: x = origin, id = 0, :373-374) */
+  double flop;             /* algorithmic FLOPs (model in spt_flops.h) */
+  double kernel_ms;        /* device time of the render kernel (HIP events) */
+} spt_stats;
+
+/* ---- host helpers mirroring the reference's host-side API ---- */
+spt_status spt_default_params(spt_params* p); /* HEAD: w=h=512, spp=16, Q=1, rr 5, light 6, ... */
+spt_status spt_camera_init(spt_camera* cam, const double lookfrom[3], const double lookat[3],
+                           const double vup[3], float vfov_deg, float aspect); /* :262-275 */
+/* rect[] :287-311 (17 primitives). *n_out = 17; fails if cap < 17. */
+spt_status spt_scene_cornell(spt_prim* out, int32_t cap, int32_t* n_out);
+/* The build-defined 32-sphere scene of config 5: room rects 0-6 of :288-294 + 32 DIFF spheres. */
+spt_status spt_scene_spheres32(spt_prim* out, int32_t cap, int32_t* n_out);
+/* Rows rendered by this shard (params tile_rows/shard_index/shard_count), ascending. Returns count. */
+int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
+
+/* ---- rendering ---- */
+/* One-shot drop-in for :528-542. rgb_out: caller-owned HOST buffer of shard_rows*w*3 floats
+ * (linear, clamped to [0,1] per channel after the spp average, :538). stats may be NULL. */
+spt_status spt_render(const spt_prim* prims, int32_t n_prims, const spt_camera* cam,
+                      const spt_params* p, float* rgb_out, spt_stats* stats);
+
+typedef struct spt_context spt_context;
+spt_status spt_context_create(int32_t device, spt_context** out);
+spt_status spt_context_destroy(spt_context* ctx);
+/* Enqueue a render on `stream` (a hipStream_t, NULL = default stream). rgb_dev: DEVICE buffer of
+ * shard_rows*w*3 floats. No host synchronisation, no allocation once the context is large enough
+ * (spt_context_reserve), so it may be captured into a hipGraph. */
+spt_status spt_context_reserve(spt_context* ctx, int32_t n_prims, const spt_params* p);
+spt_status spt_render_async(spt_context* ctx, const spt_prim* prims, int32_t n_prims,
+                            const spt_camera* cam, const spt_params* p, float* rgb_dev,
+                            void* stream);
+/* Synchronises the context's last render and returns its stats. */
+spt_status spt_context_stats(spt_context* ctx, spt_stats* out);
+
+/* ---- introspection ---- */
+int32_t spt_abi_version(void);
+const char* spt_status_string(spt_status s);
+const char* spt_last_error(void); /* thread-local text of the last failure */
+int32_t spt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPT_H_ */

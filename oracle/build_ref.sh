@@ -1,0 +1,40 @@
+#!/usr/bin/env bash
+# Build the *reference* smallpt (maurock/small-pathtracer HEAD) as a test oracle.
+#
+# TEST INFRASTRUCTURE ONLY. Compiles /root/reference/src/smallpt.cpp where it lies,
+# streaming it through sed (the patch recipe of SURVEY.md Appendix A) straight into
+# g++ via stdin: no reference source is copied into this repository or anywhere on
+# disk. Outputs go only to oracle/_ref/ (git-ignored).
+#
+# Patch (line numbers of /root/reference/src/smallpt.cpp):
+#   :424-442  delete the Q-learning early return -> the live path tracer at :444-480 runs
+#   :503      srand(time(NULL)) -> srand(seed), seed = argv[4] (default 1)
+#   :507-508  w, h, samps from argv[1..3]
+#   :517      skip create_state_space (keeps the rand() stream starting at the pixel loop)
+#   :548      output file name from argv[5]
+#   :464      (cosine variant only) q < 1  ->  q < 0
+# Pinned build: g++ -O3, x86-64 baseline (no -march=native: FMA contraction changes bits).
+set -euo pipefail
+REF=${REF:-/root/reference/src}
+OUT=${OUT:-$(cd "$(dirname "$0")" && pwd)/_ref}
+if [ ! -f "$REF/smallpt.cpp" ]; then
+  echo "reference not present at $REF; skipping oracle/_ref build" >&2
+  exit 0
+fi
+mkdir -p "$OUT"
+common_sed=(
+  -e '424,442d'
+  -e '503s/srand(time(NULL));/int seed_ = argc > 4 ? atoi(argv[4]) : 1; srand(seed_);/'
+  -e '507s/int w = 512, h = 512;/int w = argc > 1 ? atoi(argv[1]) : 512, h = argc > 2 ? atoi(argv[2]) : 512;/'
+  -e '508s/int samps = 16;/int samps = argc > 3 ? atoi(argv[3]) : 16;/'
+  -e '517s/create_state_space(dict)/0/'
+  -e '548s/"show_allrect_differentplane_red_state.ppm"/(argc > 5 ? argv[5] : "out.ppm")/'
+)
+build() {  # $1 = output binary, rest = extra sed expressions
+  local bin=$1; shift
+  sed "${common_sed[@]}" "$@" "$REF/smallpt.cpp" \
+    | g++ -O3 -w -x c++ -I"$REF" - -o "$OUT/$bin"
+}
+build smallpt_nee
+build smallpt_cos -e '464s/if (q < 1)/if (q < 0)/'
+echo "built $OUT/smallpt_nee $OUT/smallpt_cos"

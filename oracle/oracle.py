@@ -1,0 +1,141 @@
+"""ctypes front end of the CPU oracle (oracle/libspt_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker. The product package never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import importlib
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libspt_oracle.so")
+_spt = importlib.import_module("small-pathtracer_amd")
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.POINTER
+        L.spt_oracle_compat_render.argtypes = [P(_spt.spt_prim), ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_uint,
+                                               ctypes.c_int, P(ctypes.c_double)]
+        L.spt_oracle_counter_render.argtypes = [P(_spt.spt_prim), ctypes.c_int,
+                                                P(_spt.spt_camera), P(_spt.spt_params),
+                                                P(ctypes.c_int32), ctypes.c_int,
+                                                P(ctypes.c_float), P(ctypes.c_uint64), ctypes.c_int]
+        L.spt_oracle_write_ppm_d.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                             P(ctypes.c_double)]
+        L.spt_oracle_write_ppm_f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                             P(ctypes.c_float)]
+        L.spt_oracle_erand48.argtypes = [P(ctypes.c_ushort)]
+        L.spt_oracle_erand48.restype = ctypes.c_double
+        L.spt_oracle_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, P(ctypes.c_int32)]
+        L.spt_oracle_philox.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
+        L.spt_oracle_sincos2pi.argtypes = [ctypes.c_float, P(ctypes.c_float), P(ctypes.c_float)]
+        L.spt_oracle_camera.argtypes = [P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double),
+                                        P(ctypes.c_double), ctypes.c_float, ctypes.c_float]
+        L.spt_oracle_scene_cornell.argtypes = [P(_spt.spt_prim)]
+        L.spt_oracle_default_params.argtypes = [P(_spt.spt_params)]
+        L.spt_oracle_camera_spt.argtypes = [P(_spt.spt_camera), ctypes.c_float]
+        L.spt_oracle_prim_intersect.argtypes = [P(_spt.spt_prim), P(ctypes.c_double),
+                                                P(ctypes.c_double)]
+        L.spt_oracle_prim_intersect.restype = ctypes.c_double
+        L.spt_oracle_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def scene_cornell():
+    arr = (_spt.spt_prim * 17)()
+    n = lib().spt_oracle_scene_cornell(arr)
+    return [arr[i] for i in range(n)]
+
+
+def default_params(**kw):
+    p = _spt.spt_params()
+    lib().spt_oracle_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def camera(aspect: float):
+    c = _spt.spt_camera()
+    lib().spt_oracle_camera_spt(ctypes.byref(c), ctypes.c_float(aspect))
+    return c
+
+
+def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, prims=None):
+    """fp64 restatement of the reference (bit-exact with the patched oracle). (h, w, 3) float64."""
+    prims = prims or scene_cornell()
+    arr = (_spt.spt_prim * len(prims))(*prims)
+    out = np.zeros((h, w, 3), dtype=np.float64)
+    lib().spt_oracle_compat_render(arr, len(prims), w, h, spp, seed, int(nee),
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return out
+
+
+def counter_render(prims, cam, params, rows=None, threads: int = 0):
+    """Counter-mode contract on the CPU. Returns ((nrows, w, 3) float32, stats dict)."""
+    if rows is None:
+        rows = np.arange(params.height, dtype=np.int32)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    arr = (_spt.spt_prim * len(prims))(*prims)
+    out = np.zeros((len(rows), params.width, 3), dtype=np.float32)
+    st = (ctypes.c_uint64 * 8)()
+    lib().spt_oracle_counter_render(arr, len(prims), ctypes.byref(cam), ctypes.byref(params),
+                                    rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(rows),
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), st, threads)
+    return out, dict(zip(_spt.STAT_KEYS, [int(v) for v in st]))
+
+
+def write_ppm(path: str, rgb: np.ndarray) -> None:
+    h, w, _ = rgb.shape
+    if rgb.dtype == np.float64:
+        lib().spt_oracle_write_ppm_d(path.encode(), w, h,
+                                     np.ascontiguousarray(rgb).ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    else:
+        a = np.ascontiguousarray(rgb, dtype=np.float32)
+        lib().spt_oracle_write_ppm_f(path.encode(), w, h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+
+
+def erand48_seq(xi2: int, n: int):
+    xs = (ctypes.c_ushort * 3)(0, 0, xi2 & 0xFFFF)
+    return [lib().spt_oracle_erand48(xs) for _ in range(n)]
+
+
+def glibc_rand(seed: int, n: int):
+    out = (ctypes.c_int32 * n)()
+    lib().spt_oracle_glibc_rand(seed, n, out)
+    return list(out)
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().spt_oracle_philox(c, k, o)
+    return list(o)
+
+
+def sincos2pi(xi: float):
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib().spt_oracle_sincos2pi(ctypes.c_float(xi), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def threads() -> int:
+    return lib().spt_oracle_threads()

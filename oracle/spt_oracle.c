@@ -1,0 +1,769 @@
+/*
+ * spt_oracle.c — CPU ORACLE for the smallpt per-pixel sampling loop.
+ *
+ * TEST INFRASTRUCTURE ONLY. Nothing in the product links, calls or ships this file: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it, as the checker.
+ *
+ * Two restatements of /root/reference/src/smallpt.cpp (HEAD with the dead Q-learning return
+ * :424-442 removed — SURVEY.md §8c):
+ *
+ *  1. COMPAT mode (spt_oracle_compat_render): fp64, the reference's own arithmetic and RNG streams —
+ *     erand48 per image row seeded {0,0,(ushort)y^3} (:530, utilities.h:26-51) and glibc TYPE_3
+ *     rand() seeded by srand(seed) just before the pixel loop (:503, :533-534, :365-366, :460).
+ *     Built with -ffp-contract=off it reproduces the patched reference's PPM md5s bit for bit
+ *     (pinned against oracle/_ref in tests/test_oracle_golden.py and tests/golden/).
+ *
+ *  2. COUNTER mode (spt_oracle_counter_render): the device path's contract — the same algorithm in
+ *     fp32 with a counter-based Philox4x32-10 stream keyed by (seed; pixel, sample, vertex, stream),
+ *     an iterative bounce loop and fixed-point per-pixel accumulation. Every float operation is
+ *     spelled out (explicit fmaf, correctly rounded div/sqrt, own sincos polynomial) so that the HIP
+ *     kernel must reproduce it BIT-EXACTLY. See DESIGN.md "Counter-mode contract".
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/spt.h"
+#include "../include/spt_flops.h"
+
+/* ========================================================================================== */
+/* COMPAT MODE (fp64)                                                                          */
+/* ========================================================================================== */
+
+typedef struct { double x, y, z; } dv; /* Vec :24-62 */
+
+static inline dv dv3(double x, double y, double z) { dv r = {x, y, z}; return r; }
+static inline dv dadd(dv a, dv b) { return dv3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline dv dsub(dv a, dv b) { return dv3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline dv dmul(dv a, double b) { return dv3(a.x * b, a.y * b, a.z * b); }
+static inline dv dmulv(dv a, dv b) { return dv3(a.x * b.x, a.y * b.y, a.z * b.z); } /* mult :47 */
+static inline double ddot(dv a, dv b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* :53 */
+static inline dv dcross(dv a, dv b) { /* operator% :56-58 */
+  return dv3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline dv dnorm(dv a) { return dmul(a, 1 / sqrt(a.x * a.x + a.y * a.y + a.z * a.z)); } /* :50 */
+
+/* erand48 of utilities.h:26-51: x <- 0x5DEECE66D*x + 0xB mod 2^48, value x/2^48. */
+static double o_erand48(unsigned short xs[3]) {
+  uint64_t x = (uint64_t)xs[0] | ((uint64_t)xs[1] << 16) | ((uint64_t)xs[2] << 32);
+  x = (x * 0x5DEECE66Dull + 0xBull) & 0xFFFFFFFFFFFFull;
+  xs[0] = (unsigned short)x;
+  xs[1] = (unsigned short)(x >> 16);
+  xs[2] = (unsigned short)(x >> 32);
+  return ldexp((double)xs[0], -48) + ldexp((double)xs[1], -32) + ldexp((double)xs[2], -16);
+}
+
+/* glibc random_r TYPE_3 (x^31 + x^3 + 1 additive feedback), i.e. what srand()/rand() compute.
+ * Restated from the published algorithm (glibc stdlib/random_r.c, srandom_r + random_r). */
+typedef struct { int32_t r[34]; int i; } o_glibc_rand;
+static void o_srand(o_glibc_rand* g, unsigned seed) {
+  int32_t r[344 + 34];
+  int k;
+  if (seed == 0) seed = 1;
+  r[0] = (int32_t)seed;
+  for (k = 1; k < 31; k++) {
+    const int32_t hi = r[k - 1] / 127773, lo = r[k - 1] % 127773;
+    int32_t word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    r[k] = word;
+  }
+  for (k = 31; k < 34; k++) r[k] = r[k - 31];
+  for (k = 34; k < 344; k++) r[k] = (int32_t)((uint32_t)r[k - 31] + (uint32_t)r[k - 3]);
+  for (k = 0; k < 34; k++) g->r[k] = r[310 + k]; /* last 34 values r[310..343] */
+  g->i = 0;                                      /* ring index of r[310] */
+}
+static int32_t o_rand(o_glibc_rand* g) {
+  /* r[n] = r[n-31] + r[n-3]; ring of the last 34 values, g->i points at r[n-34]. */
+  const int i = g->i;
+  const uint32_t v = (uint32_t)g->r[(i + 3) % 34] + (uint32_t)g->r[(i + 31) % 34];
+  g->r[i] = (int32_t)v;
+  g->i = (i + 1) % 34;
+  return (int32_t)(v >> 1);
+}
+#define O_RAND_MAX 2147483647
+
+typedef struct { int kind; double g[5]; dv e, c; } o_prim;
+
+/* Rectangle_*::intersect :102-112, :145-155, :188-198 and Sphere::intersect :229-239. */
+static double o_prim_intersect(const o_prim* P, dv o, dv d) {
+  double t;
+  float a, b;
+  switch (P->kind) {
+    case SPT_RECT_XZ: /* (x1,x2,z1,z2,y) */
+      t = (P->g[4] - o.y) / d.y;
+      a = (float)(o.x + d.x * t);
+      b = (float)(o.z + d.z * t);
+      if (a < P->g[0] || a > P->g[1] || b < P->g[2] || b > P->g[3] || t < 0) return 0;
+      return t;
+    case SPT_RECT_XY: /* (x1,x2,y1,y2,z) */
+      t = (P->g[4] - o.z) / d.z;
+      a = (float)(o.x + d.x * t);
+      b = (float)(o.y + d.y * t);
+      if (a < P->g[0] || a > P->g[1] || b < P->g[2] || b > P->g[3] || t < 0) return 0;
+      return t;
+    case SPT_RECT_YZ: /* (y1,y2,z1,z2,x) */
+      t = (P->g[4] - o.x) / d.x;
+      a = (float)(o.y + d.y * t);
+      b = (float)(o.z + d.z * t);
+      if (a < P->g[0] || a > P->g[1] || b < P->g[2] || b > P->g[3] || t < 0) return 0;
+      return t;
+    default: { /* SPHERE (rad, px, py, pz) */
+      const dv op = dsub(dv3(P->g[1], P->g[2], P->g[3]), o);
+      const double eps = 1e-4, bb = ddot(op, d);
+      double det = bb * bb - ddot(op, op) + P->g[0] * P->g[0];
+      if (det < 0) return 0;
+      det = sqrt(det);
+      return (t = bb - det) > eps ? t : ((t = bb + det) > eps ? t : 0);
+    }
+  }
+}
+
+typedef struct {
+  const o_prim* prims;
+  int n;
+  int light_id;
+  int nee; /* 1: `q < 1` (HEAD :464), 0: `q < 0` (cosine-only) */
+  o_glibc_rand* g;
+} o_scene;
+
+/* intersect :323-335: strict `<` keeps the lowest index on ties; id untouched on a miss. */
+static int o_intersect(const o_scene* S, dv o, dv d, double* t, int* id) {
+  const double inf = *t = 1e20;
+  int i;
+  for (i = 0; i < S->n; i++) {
+    const double dd = o_prim_intersect(&S->prims[i], o, d);
+    if (dd != 0 && dd < *t) { *t = dd; *id = i; }
+  }
+  return *t < inf;
+}
+
+/* Hitable::normal :118-124 etc: geometric normal oriented against the ray. */
+static dv o_normal(const o_prim* P, dv d, dv x) {
+  dv n;
+  switch (P->kind) {
+    case SPT_RECT_XZ: n = dv3(0, 1, 0); break;
+    case SPT_RECT_XY: n = dv3(0, 0, 1); break;
+    case SPT_RECT_YZ: n = dv3(1, 0, 0); break;
+    default: n = dnorm(dsub(x, dv3(P->g[1], P->g[2], P->g[3]))); break;
+  }
+  return ddot(n, d) < 0 ? n : dmul(n, (double)-1); /* n * -1 : Vec::operator*(int) */
+}
+
+/* random_scattering :337-348 (cosine-weighted). */
+static dv o_random_scattering(dv nl, unsigned short* Xi) {
+  const double r1 = 2 * M_PI * o_erand48(Xi);
+  const double r2 = o_erand48(Xi);
+  const double r2s = sqrt(r2);
+  const dv w = nl;
+  const dv u = dnorm(dcross(fabs(w.x) > .1 ? dv3(0, 1, 0) : dv3(1, 0, 0), w));
+  const dv v = dcross(w, u);
+  return dnorm(dadd(dadd(dmul(dmul(u, cos(r1)), r2s), dmul(dmul(v, sin(r1)), r2s)),
+                    dmul(w, sqrt(1 - r2))));
+}
+
+/* light_sampling :363-369. rand()*36 is int arithmetic (wraps with glibc RAND_MAX=2^31-1). */
+static dv o_light_sampling(const o_scene* S, dv hit) {
+  const int32_t ax = (int32_t)((uint32_t)o_rand(S->g) * 36u);
+  const double x_light = 32 + ax / (double)O_RAND_MAX;
+  const int32_t az = (int32_t)((uint32_t)o_rand(S->g) * 36u);
+  const double z_light = 63 + az / (double)O_RAND_MAX;
+  return dsub(dv3(x_light, 81.6, z_light), hit);
+}
+
+/* radiance :419-480 (live path), recursive exactly as the reference (evaluation order matters). */
+static dv o_radiance(const o_scene* S, dv ro, dv rd, int depth, unsigned short* Xi) {
+  int id = 0;
+  double t;
+  dv x;
+  if (!o_intersect(S, ro, rd, &t, &id)) x = dv3(0, 0, 0); /* hittingPoint :371-377 */
+  else x = dadd(ro, dmul(rd, t));
+  {
+    const o_prim* obj = &S->prims[id];
+    const dv nl = o_normal(obj, rd, x);
+    dv f = obj->c;
+    const double p = f.x > f.y && f.x > f.z ? f.x : f.y > f.z ? f.y : f.z;
+    dv d;
+    double q, PDF_inverse = 1, BRDF = 1;
+    if (++depth > 5 || !p) {
+      if (o_erand48(Xi) < p) f = dmul(f, 1 / p);
+      else return obj->e;
+    }
+    q = o_rand(S->g) / (double)O_RAND_MAX;
+    if (S->nee ? (q < 1) : (q < 0)) {
+      d = o_light_sampling(S, x);
+      d = dnorm(d);
+      o_intersect(S, x, d, &t, &id);
+      if (id != S->light_id) {
+        d = o_random_scattering(nl, Xi);
+        d = dnorm(d);
+        o_intersect(S, x, d, &t, &id);
+      } else {
+        d = dnorm(d);
+        PDF_inverse = fabs((1296 * ddot(d, dv3(0, 1, 0))) / (t * t));
+        d = dnorm(d);
+        BRDF = fabs(ddot(d, nl) / M_PI);
+      }
+    } else {
+      d = o_random_scattering(nl, Xi);
+      d = dnorm(d);
+      o_intersect(S, x, d, &t, &id);
+    }
+    d = dnorm(d);
+    {
+      const dv Li = o_radiance(S, x, d, depth, Xi);
+      return dadd(obj->e, dmul(dmul(dmulv(f, Li), PDF_inverse), BRDF));
+    }
+  }
+}
+
+static o_prim o_from_spt(const spt_prim* s) {
+  o_prim p;
+  p.kind = s->kind;
+  memcpy(p.g, s->geom, sizeof p.g);
+  p.e = dv3(s->e[0], s->e[1], s->e[2]);
+  p.c = dv3(s->c[0], s->c[1], s->c[2]);
+  return p;
+}
+
+/* Camera ctor :262-275 (theta/half_height float, tan(float) resolves to tanf under libstdc++). */
+void spt_oracle_camera(double out[12], const double lf[3], const double la[3], const double vup[3],
+                       float vfov, float aspect) {
+  const float theta = (float)(vfov * M_PI / 180);
+  const float half_height = tanf(theta / 2);
+  const float half_width = aspect * half_height;
+  const dv origin = dv3(lf[0], lf[1], lf[2]);
+  const dv w = dnorm(dsub(dv3(la[0], la[1], la[2]), origin));
+  const dv u = dnorm(dcross(w, dv3(vup[0], vup[1], vup[2])));
+  const dv v = dcross(u, w);
+  const dv llc = dadd(dsub(dsub(origin, dmul(u, (double)half_width)), dmul(v, (double)half_height)), w);
+  const dv hor = dmul(u, (double)(half_width * 2));
+  const dv ver = dmul(v, (double)(half_height * 2));
+  const double vals[12] = {origin.x, origin.y, origin.z, llc.x, llc.y, llc.z,
+                           hor.x,    hor.y,    hor.z,    ver.x, ver.y, ver.z};
+  memcpy(out, vals, sizeof vals);
+}
+
+/* main() :502-542 with the HEAD scene, srand(seed) and the state-space build skipped.
+ * c_out: w*h*3 doubles (clamped, row-major, y=0 top). Returns 0. */
+int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp, unsigned seed,
+                             int nee, double* c_out) {
+  o_prim* P = (o_prim*)malloc(sizeof(o_prim) * (size_t)n);
+  o_glibc_rand g;
+  o_scene S;
+  double cam[12];
+  const double lf[3] = {50, 40, 168}, la[3] = {50, 40, 5}, up[3] = {0, 1, 0};
+  int i, y;
+  dv origin, llc, hor, ver;
+  for (i = 0; i < n; i++) P[i] = o_from_spt(&prims[i]);
+  S.prims = P; S.n = n; S.light_id = 6; S.nee = nee; S.g = &g;
+  o_srand(&g, seed);
+  spt_oracle_camera(cam, lf, la, up, 65, (float)w / (float)h);
+  origin = dv3(cam[0], cam[1], cam[2]);
+  llc = dv3(cam[3], cam[4], cam[5]);
+  hor = dv3(cam[6], cam[7], cam[8]);
+  ver = dv3(cam[9], cam[10], cam[11]);
+  for (y = 0, i = 0; y < h; y++) {
+    unsigned short x, Xi[3];
+    Xi[0] = 0; Xi[1] = 0; Xi[2] = (unsigned short)(y * y * y);
+    for (x = 0; x < w; x++) {
+      dv r = dv3(0, 0, 0);
+      int s;
+      for (s = 0; s < spp; s++) {
+        const float u = (float)(x - 0.5 + o_rand(&g) / (double)O_RAND_MAX) / (float)w;
+        const float v = (float)((h - y - 1) - 0.5 + o_rand(&g) / (double)O_RAND_MAX) / (float)h;
+        const dv d = dsub(dadd(dadd(llc, dmul(hor, (double)u)), dmul(ver, (double)v)), origin);
+        const dv L = o_radiance(&S, origin, dnorm(d), 0, Xi);
+        r = dadd(r, dmul(L, 1. / spp));
+      }
+      c_out[3 * i + 0] = r.x < 0 ? 0 : r.x > 1 ? 1 : r.x;
+      c_out[3 * i + 1] = r.y < 0 ? 0 : r.y > 1 ? 1 : r.y;
+      c_out[3 * i + 2] = r.z < 0 ? 0 : r.z > 1 ? 1 : r.z;
+      i++;
+    }
+  }
+  free(P);
+  return 0;
+}
+
+/* toInt :319-321 + the P3 writer :548-551 (byte-identical format). */
+static int o_toInt(double x) { return (int)(pow(x < 0 ? 0 : x > 1 ? 1 : x, 1 / 2.2) * 255 + .5); }
+int spt_oracle_write_ppm_d(const char* path, int w, int h, const double* c) {
+  FILE* f = fopen(path, "w");
+  int i;
+  if (!f) return 1;
+  fprintf(f, "P3\n%d %d\n%d\n", w, h, 255);
+  for (i = 0; i < w * h; i++)
+    fprintf(f, "%d %d %d ", o_toInt(c[3 * i]), o_toInt(c[3 * i + 1]), o_toInt(c[3 * i + 2]));
+  fclose(f);
+  return 0;
+}
+int spt_oracle_write_ppm_f(const char* path, int w, int h, const float* c) {
+  FILE* f = fopen(path, "w");
+  int i;
+  if (!f) return 1;
+  fprintf(f, "P3\n%d %d\n%d\n", w, h, 255);
+  for (i = 0; i < w * h; i++)
+    fprintf(f, "%d %d %d ", o_toInt(c[3 * i]), o_toInt(c[3 * i + 1]), o_toInt(c[3 * i + 2]));
+  fclose(f);
+  return 0;
+}
+
+/* Exposed for known-answer tests. */
+double spt_oracle_erand48(unsigned short xs[3]) { return o_erand48(xs); }
+void spt_oracle_glibc_rand(unsigned seed, int n, int32_t* out) {
+  o_glibc_rand g;
+  int i;
+  o_srand(&g, seed);
+  for (i = 0; i < n; i++) out[i] = o_rand(&g);
+}
+double spt_oracle_prim_intersect(const spt_prim* s, const double o[3], const double d[3]) {
+  const o_prim p = o_from_spt(s);
+  return o_prim_intersect(&p, dv3(o[0], o[1], o[2]), dv3(d[0], d[1], d[2]));
+}
+
+/* ========================================================================================== */
+/* COUNTER MODE (fp32) — the device contract                                                   */
+/* ========================================================================================== */
+
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 constants). */
+#define PH_M0 0xD2511F53u
+#define PH_M1 0xCD9E8D57u
+#define PH_W0 0x9E3779B9u
+#define PH_W1 0xBB67AE85u
+void spt_oracle_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  int r;
+  for (r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)PH_M0 * c0, p1 = (uint64_t)PH_M1 * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += PH_W0;
+    k1 += PH_W1;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+typedef struct { float x, y, z; } fv;
+static inline fv fv3(float x, float y, float z) { fv r = {x, y, z}; return r; }
+static inline float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
+static inline float fdot(fv a, fv b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline fv fnormalize(fv v) {
+  const float inv = 1.0f / sqrtf(fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x)));
+  return fv3(v.x * inv, v.y * inv, v.z * inv);
+}
+static inline fv fcross(fv a, fv b) {
+  return fv3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+/* sin(2*pi*xi), cos(2*pi*xi) for xi in [0,1): exact quarter-turn reduction + Taylor polynomials
+ * in r = 4*xi - k (|r| <= 1/2, i.e. |theta| <= pi/4). Coefficients (pi/2)^n/n!. */
+#define SC_S1 1.57079632679489662f
+#define SC_S3 -0.645964097506246254f
+#define SC_S5 0.0796926262461670451f
+#define SC_S7 -0.00468175413531868810f
+#define SC_S9 0.000160441184787359821f
+#define SC_C2 -1.23370055013616983f
+#define SC_C4 0.253669507901048014f
+#define SC_C6 -0.0208634807633529609f
+#define SC_C8 0.000919260274839426030f
+void spt_oracle_sincos2pi(float xi, float* s_out, float* c_out) {
+  const float q = xi * 4.0f;
+  const float kf = rintf(q);
+  const float r = q - kf;
+  const int k = (int)kf & 3;
+  const float r2 = r * r;
+  float ps = fmaf(r2, SC_S9, SC_S7), pc = fmaf(r2, SC_C8, SC_C6), s, c;
+  ps = fmaf(r2, ps, SC_S5);
+  ps = fmaf(r2, ps, SC_S3);
+  ps = fmaf(r2, ps, SC_S1);
+  s = r * ps;
+  pc = fmaf(r2, pc, SC_C4);
+  pc = fmaf(r2, pc, SC_C2);
+  c = fmaf(r2, pc, 1.0f);
+  switch (k) {
+    case 0: *s_out = s; *c_out = c; break;
+    case 1: *s_out = c; *c_out = -s; break;
+    case 2: *s_out = -s; *c_out = -c; break;
+    default: *s_out = -c; *c_out = s; break;
+  }
+}
+
+typedef struct {
+  int kind;
+  float k, b1, b2, c1, c2; /* rect: plane k, in-plane bounds; sphere: k=rad^2 (unused), b1..: p */
+  float rad2, px, py, pz;
+  fv e, c;
+  float pmax;
+} c_prim;
+
+typedef struct {
+  const c_prim* prims;
+  int n;
+  const spt_params* P;
+  uint32_t key[2];
+} c_ctx;
+
+/* The counter-mode scene intersection. inv = 1/d computed once per ray; ties keep the lowest index;
+ * id is left untouched on a miss; returns 1 on hit with *t set, *t = 1e20f on a miss. */
+static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
+  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  float tmin = 1e20f;
+  int i;
+  for (i = 0; i < C->n; i++) {
+    const c_prim* P = &C->prims[i];
+    float tt, a, b;
+    switch (P->kind) {
+      case SPT_RECT_XY:
+        tt = (P->k - o.z) * iz; a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y); break;
+      case SPT_RECT_XZ:
+        tt = (P->k - o.y) * iy; a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z); break;
+      case SPT_RECT_YZ:
+        tt = (P->k - o.x) * ix; a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z); break;
+      default: { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
+        const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
+        const float bb = fdot(op, d);
+        const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+        const float det = P->rad2 - fdot(q, q);
+        float sd, t1, t2;
+        if (!(det >= 0.0f)) continue;
+        sd = sqrtf(det);
+        t1 = bb - sd;
+        t2 = bb + sd;
+        tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+        if (tt != 0.0f && tt < tmin) { tmin = tt; *id = i; }
+        continue;
+      }
+    }
+    /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin; for finite
+     * a, b (always, once tt < tmin) that is exactly the conjunction below. */
+    if (a >= P->b1 && a <= P->b2 && b >= P->c1 && b <= P->c2 && tt > 0.0f && tt < tmin) {
+      tmin = tt;
+      *id = i;
+    }
+  }
+  *t = tmin;
+  return tmin < 1e20f;
+}
+
+static fv c_cosine(fv nl, uint32_t ra, uint32_t rb) {
+  const float xi1 = u01(ra), xi2 = u01(rb);
+  float s, c;
+  fv a, u, v;
+  float r2s, s1, cr, sr;
+  spt_oracle_sincos2pi(xi1, &s, &c);
+  r2s = sqrtf(xi2);
+  s1 = sqrtf(1.0f - xi2);
+  a = fabsf(nl.x) > 0.1f ? fv3(nl.z, 0.0f, -nl.x) : fv3(0.0f, -nl.z, nl.y);
+  u = fnormalize(a);
+  v = fcross(nl, u);
+  cr = c * r2s;
+  sr = s * r2s;
+  return fnormalize(fv3(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)),
+                        fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
+                        fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr))));
+}
+
+typedef struct {
+  uint64_t samples, path_rays, shadow_rays, vertices, nee_events, nee_light_hits, cosine_samples,
+      misses;
+} c_stats;
+
+/* One path of the counter-mode contract; returns L. */
+static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const float cam[12],
+                 c_stats* st) {
+  const spt_params* P = C->P;
+  uint32_t ctr[4], r[4];
+  fv o, d, T = fv3(1, 1, 1), L = fv3(0, 0, 0);
+  int depth = 0, carried = 0, c_hit = 0, c_id = 0;
+  float c_t = 0;
+  ctr[0] = pix; ctr[1] = s; ctr[2] = 0; ctr[3] = 0;
+  spt_oracle_philox(ctr, C->key, r);
+  {
+    const float su = (((float)px - 0.5f) + u01(r[0])) / (float)P->width;
+    const float sv = (((float)(P->height - py - 1) - 0.5f) + u01(r[1])) / (float)P->height;
+    o = fv3(cam[0], cam[1], cam[2]);
+    d = fnormalize(fv3(fmaf(cam[9], sv, fmaf(cam[6], su, cam[3])) - cam[0],
+                       fmaf(cam[10], sv, fmaf(cam[7], su, cam[4])) - cam[1],
+                       fmaf(cam[11], sv, fmaf(cam[8], su, cam[5])) - cam[2]));
+  }
+  st->samples++;
+  for (;;) {
+    int id = 0, hit;
+    float t;
+    fv x, nl, f, e;
+    const c_prim* H;
+    if (carried) {
+      hit = c_hit; t = c_t; id = hit ? c_id : 0;
+      carried = 0;
+    } else {
+      hit = c_intersect(C, o, d, &t, &id);
+      st->path_rays++;
+    }
+    H = &C->prims[id];
+    if (!hit) { x = fv3(0, 0, 0); st->misses++; }
+    else {
+      /* hittingPoint :375 x = o + d*t with the plane distance re-derived as the reference does
+       * (:103, (k - o_a)/d_a, one correctly rounded division per vertex, then mul + add): this
+       * sets how often x lands beyond the plane, i.e. the reference's self-hit/leak rate. */
+      float tr = t;
+      if (H->kind == SPT_RECT_XY) tr = (H->k - o.z) / d.z;
+      else if (H->kind == SPT_RECT_XZ) tr = (H->k - o.y) / d.y;
+      else if (H->kind == SPT_RECT_YZ) tr = (H->k - o.x) / d.x;
+      x = fv3(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
+    }
+    st->vertices++;
+    switch (H->kind) {
+      case SPT_RECT_XY: nl = d.z < 0.0f ? fv3(0, 0, 1) : fv3(0, 0, -1); break;
+      case SPT_RECT_XZ: nl = d.y < 0.0f ? fv3(0, 1, 0) : fv3(0, -1, 0); break;
+      case SPT_RECT_YZ: nl = d.x < 0.0f ? fv3(1, 0, 0) : fv3(-1, 0, 0); break;
+      default: {
+        const fv n = fnormalize(fv3(x.x - H->px, x.y - H->py, x.z - H->pz));
+        nl = fdot(n, d) < 0.0f ? n : fv3(-n.x, -n.y, -n.z);
+      }
+    }
+    f = H->c;
+    e = H->e;
+    ++depth;
+    {
+      const float p = H->pmax;
+      int term = 0;
+      if (P->max_depth > 0 && depth >= P->max_depth) term = 1;
+      else if (depth > P->rr_depth || p == 0.0f) {
+        if (!(p > 0.0f)) term = 1;
+        else {
+          int keep = 1;
+          if (p < 1.0f) {
+            ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 1;
+            spt_oracle_philox(ctr, C->key, r);
+            keep = u01(r[0]) < p;
+          }
+          if (keep) {
+            const float ip = 1.0f / p;
+            f = fv3(f.x * ip, f.y * ip, f.z * ip);
+          } else term = 1;
+        }
+      }
+      if (term) {
+        L = fv3(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+        return L;
+      }
+    }
+    {
+      int nee;
+      float w = 1.0f;
+      fv dn;
+      if (P->nee_prob >= 1.0f) nee = 1;
+      else if (P->nee_prob <= 0.0f) nee = 0;
+      else {
+        ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 1;
+        spt_oracle_philox(ctr, C->key, r);
+        nee = u01(r[1]) < P->nee_prob;
+      }
+      ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 0;
+      spt_oracle_philox(ctr, C->key, r);
+      if (nee) {
+        float xl, zl, ts;
+        int ids = id, sh;
+        fv dl;
+        if (P->light_mode == SPT_LIGHT_GLIBC_WRAP) {
+          const uint32_t dxi = (uint32_t)P->light_dx, dzi = (uint32_t)P->light_dz;
+          xl = fmaf((float)(int32_t)((r[0] >> 1) * dxi), 0x1p-31f, P->light_x0);
+          zl = fmaf((float)(int32_t)((r[1] >> 1) * dzi), 0x1p-31f, P->light_z0);
+        } else {
+          xl = fmaf(u01(r[0]), P->light_dx, P->light_x0);
+          zl = fmaf(u01(r[1]), P->light_dz, P->light_z0);
+        }
+        dl = fnormalize(fv3(xl - x.x, P->light_y - x.y, zl - x.z));
+        sh = c_intersect(C, x, dl, &ts, &ids);
+        st->nee_events++;
+        st->shadow_rays++;
+        if (ids == P->light_id) {
+          const float pdf = fabsf((P->light_area * dl.y) / (ts * ts));
+          const float brdf = fabsf(fdot(dl, nl) * 0.318309886183790672f);
+          st->nee_light_hits++;
+          w = pdf * brdf;
+          dn = dl;
+          carried = 1; c_hit = sh; c_t = ts; c_id = ids;
+        } else {
+          dn = c_cosine(nl, r[2], r[3]);
+          st->cosine_samples++;
+        }
+      } else {
+        dn = c_cosine(nl, r[2], r[3]);
+        st->cosine_samples++;
+      }
+      L = fv3(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+      T = fv3((T.x * f.x) * w, (T.y * f.y) * w, (T.z * f.z) * w);
+      o = x;
+      d = dn;
+    }
+  }
+}
+
+static inline uint64_t c_fix(float L, float inv_spp) {
+  float c = L * inv_spp;
+  if (!(c >= 0.0f)) c = 0.0f;
+  if (c > 1.0f) c = 1.0f;
+  return (uint64_t)(c * 4294967296.0f);
+}
+
+static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
+  int i;
+  for (i = 0; i < n; i++) {
+    c_prim* P = &out[i];
+    memset(P, 0, sizeof *P);
+    P->kind = s[i].kind;
+    if (s[i].kind == SPT_SPHERE) {
+      P->rad2 = (float)s[i].geom[0] * (float)s[i].geom[0];
+      P->px = (float)s[i].geom[1]; P->py = (float)s[i].geom[2]; P->pz = (float)s[i].geom[3];
+    } else {
+      P->b1 = (float)s[i].geom[0]; P->b2 = (float)s[i].geom[1];
+      P->c1 = (float)s[i].geom[2]; P->c2 = (float)s[i].geom[3];
+      P->k = (float)s[i].geom[4];
+    }
+    P->e = fv3((float)s[i].e[0], (float)s[i].e[1], (float)s[i].e[2]);
+    P->c = fv3((float)s[i].c[0], (float)s[i].c[1], (float)s[i].c[2]);
+    P->pmax = P->c.x > P->c.y && P->c.x > P->c.z ? P->c.x : P->c.y > P->c.z ? P->c.y : P->c.z;
+  }
+}
+
+/* Render the rows listed in rows[0..nrows) (image row indices, y=0 top) of the counter-mode contract.
+ * rgb_out: nrows*w*3 floats. stats_out: 8 uint64 in spt_stats order (may be NULL).
+ * threads <= 0: all OpenMP threads. Deterministic for any thread count. */
+int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* cam,
+                              const spt_params* P, const int32_t* rows, int nrows, float* rgb_out,
+                              uint64_t* stats_out, int threads) {
+  c_prim* CP = (c_prim*)malloc(sizeof(c_prim) * (size_t)n);
+  c_ctx C;
+  float camf[12];
+  const float inv_spp = 1.0f / (float)P->spp;
+  c_stats tot;
+  int i, ri;
+  memset(&tot, 0, sizeof tot);
+  c_prims_from_spt(prims, n, CP);
+  C.prims = CP; C.n = n; C.P = P; C.key[0] = P->seed; C.key[1] = SPT_PHILOX_KEY1;
+  for (i = 0; i < 3; i++) {
+    camf[i] = (float)cam->origin[i];
+    camf[3 + i] = (float)cam->lower_left_corner[i];
+    camf[6 + i] = (float)cam->horizontal[i];
+    camf[9 + i] = (float)cam->vertical[i];
+  }
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#else
+  (void)threads;
+#endif
+#pragma omp parallel
+  {
+    c_stats st;
+    memset(&st, 0, sizeof st);
+#pragma omp for schedule(dynamic, 1)
+    for (ri = 0; ri < nrows; ri++) {
+      const int y = rows[ri];
+      int x;
+      for (x = 0; x < P->width; x++) {
+        const uint32_t pix = (uint32_t)y * (uint32_t)P->width + (uint32_t)x;
+        uint64_t acc[3] = {0, 0, 0};
+        int s, ch;
+        for (s = 0; s < P->spp; s++) {
+          const fv L = c_path(&C, pix, (uint32_t)s, x, y, camf, &st);
+          acc[0] += c_fix(L.x, inv_spp);
+          acc[1] += c_fix(L.y, inv_spp);
+          acc[2] += c_fix(L.z, inv_spp);
+        }
+        for (ch = 0; ch < 3; ch++) {
+          float v = (float)acc[ch] * 0x1p-32f;
+          rgb_out[((size_t)ri * (size_t)P->width + (size_t)x) * 3 + (size_t)ch] = v > 1.0f ? 1.0f : v;
+        }
+      }
+    }
+#pragma omp critical
+    {
+      tot.samples += st.samples; tot.path_rays += st.path_rays; tot.shadow_rays += st.shadow_rays;
+      tot.vertices += st.vertices; tot.nee_events += st.nee_events;
+      tot.nee_light_hits += st.nee_light_hits; tot.cosine_samples += st.cosine_samples;
+      tot.misses += st.misses;
+    }
+  }
+  if (stats_out) {
+    stats_out[0] = tot.samples; stats_out[1] = tot.path_rays; stats_out[2] = tot.shadow_rays;
+    stats_out[3] = tot.vertices; stats_out[4] = tot.nee_events; stats_out[5] = tot.nee_light_hits;
+    stats_out[6] = tot.cosine_samples; stats_out[7] = tot.misses;
+  }
+  free(CP);
+  return 0;
+}
+
+int spt_oracle_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* ========================================================================================== */
+/* Oracle-side scene / params (restated independently of the product's host helpers)           */
+/* ========================================================================================== */
+
+static void o_set(spt_prim* p, int kind, double a, double b, double c, double d, double k, double e,
+                  double cr, double cg, double cb) {
+  memset(p, 0, sizeof *p);
+  p->kind = kind; p->refl = SPT_DIFF;
+  p->geom[0] = a; p->geom[1] = b; p->geom[2] = c; p->geom[3] = d; p->geom[4] = k;
+  p->e[0] = p->e[1] = p->e[2] = e;
+  p->c[0] = cr; p->c[1] = cg; p->c[2] = cb;
+}
+
+/* rect[] of :287-311. */
+int spt_oracle_scene_cornell(spt_prim* o) {
+  o_set(&o[0], SPT_RECT_XY, 1, 99, 0, 81.6, 0, 0, .75, .75, .75);    /* Front  :288 */
+  o_set(&o[1], SPT_RECT_XY, 1, 99, 0, 81.6, 170, 0, .75, .75, .75);  /* Back   :289 */
+  o_set(&o[2], SPT_RECT_YZ, 0, 81.6, 0, 170, 1, 0, .25, .75, .25);   /* Left   :290 */
+  o_set(&o[3], SPT_RECT_YZ, 0, 81.6, 0, 170, 99, 0, .75, .25, .25);  /* Right  :291 */
+  o_set(&o[4], SPT_RECT_XZ, 1, 99, 0, 170, 0, 0, .75, .75, .75);     /* Bottom :292 */
+  o_set(&o[5], SPT_RECT_XZ, 1, 99, 0, 170, 81.6, 0, .75, .75, .75);  /* Top    :293 */
+  o_set(&o[6], SPT_RECT_XZ, 32, 68, 63, 96, 81.5, 12, 0, 0, 0);      /* Light  :294 */
+  o_set(&o[7], SPT_RECT_XY, 12, 42, 0, 50, 32, 0, 1, 1, 1);          /* Tall box :300-304 */
+  o_set(&o[8], SPT_RECT_XY, 12, 42, 0, 50, 62, 0, 1, 1, 1);
+  o_set(&o[9], SPT_RECT_YZ, 0, 50, 32, 62, 12, 0, 1, 1, 1);
+  o_set(&o[10], SPT_RECT_YZ, 0, 50, 32, 62, 42, 0, 1, 1, 1);
+  o_set(&o[11], SPT_RECT_XZ, 12, 42, 32, 62, 50, 0, 1, 1, 1);
+  o_set(&o[12], SPT_RECT_XY, 63, 88, 0, 25, 63, 0, 1, 1, 1);         /* Short box :306-310 */
+  o_set(&o[13], SPT_RECT_XY, 63, 88, 0, 25, 88, 0, 1, 1, 1);
+  o_set(&o[14], SPT_RECT_YZ, 0, 25, 63, 88, 63, 0, 1, 1, 1);
+  o_set(&o[15], SPT_RECT_YZ, 0, 25, 63, 88, 88, 0, 1, 1, 1);
+  o_set(&o[16], SPT_RECT_XZ, 63, 88, 63, 88, 25, 0, 1, 1, 1);
+  return 17;
+}
+
+/* HEAD constants: :507-508 (512x512 @ 16), :464 (Q=1), :448 (5), :467 (6), :365-367, :471. */
+void spt_oracle_default_params(spt_params* p) {
+  memset(p, 0, sizeof *p);
+  p->width = 512; p->height = 512; p->spp = 16; p->seed = 1;
+  p->nee_prob = 1.0f; p->rr_depth = 5; p->max_depth = 0; p->light_id = 6;
+  p->light_x0 = 32; p->light_dx = 36; p->light_z0 = 63; p->light_dz = 36;
+  p->light_y = 81.6f; p->light_area = 1296; p->light_mode = SPT_LIGHT_GLIBC_WRAP;
+  p->tile_rows = 8; p->shard_index = 0; p->shard_count = 1;
+}
+
+void spt_oracle_camera_spt(spt_camera* c, float aspect) {
+  double v[12];
+  const double lf[3] = {50, 40, 168}, la[3] = {50, 40, 5}, up[3] = {0, 1, 0};
+  int i;
+  spt_oracle_camera(v, lf, la, up, 65, aspect);
+  for (i = 0; i < 3; i++) {
+    c->origin[i] = v[i]; c->lower_left_corner[i] = v[3 + i];
+    c->horizontal[i] = v[6 + i]; c->vertical[i] = v[9 + i];
+  }
+}

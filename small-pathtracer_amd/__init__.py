@@ -1,0 +1,352 @@
+"""small-pathtracer_amd — MI355X-native drop-in for the smallpt per-pixel sampling loop.
+
+Python mirror of the reference's host API over the C ABI in ``include/spt.h`` (libspt.so):
+
+=====================================  ==================================================
+reference (/root/reference/src/...)    here
+=====================================  ==================================================
+``Rectangle_xz/xy/yz`` smallpt.cpp:92-221  ``Rectangle_xz/xy/yz`` (same ctor argument order)
+``Sphere`` :223-254                     ``Sphere``
+``Refl_t {DIFF, SPEC, REFR}`` :72-74    ``DIFF, SPEC, REFR``
+``Camera`` :256-285                     ``Camera`` (constructor semantics via spt_camera_init)
+``Hitable *rect[]`` :287-311            ``cornell_scene()``
+``clamp``/``toInt`` :314-321            ``clamp``/``toInt``
+pixel loop :528-542 (+ radiance :419)   ``render()`` / ``Renderer`` (HIP kernel, gfx950)
+PPM writer :548-551                     ``write_ppm()`` (byte-identical P3)
+=====================================  ==================================================
+
+The product path is the HIP kernel only: ``render()`` raises if libspt.so or a gfx950 device is
+missing — there is no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspt.so")
+
+DIFF, SPEC, REFR = 0, 1, 2
+RECT_XY, RECT_XZ, RECT_YZ, SPHERE = 0, 1, 2, 3
+LIGHT_GLIBC_WRAP, LIGHT_UNIFORM = 0, 1
+PHILOX_KEY1 = 0x53505431
+
+STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "no usable gfx950 device",
+          4: "device out of memory", 5: "unsupported feature"}
+
+
+class SptError(RuntimeError):
+    def __init__(self, status: int, msg: str = ""):
+        super().__init__(f"spt error {status} ({STATUS.get(status, '?')}): {msg}")
+        self.status = status
+
+
+# ---------------------------------------------------------------------------------------------
+# ctypes mirror of include/spt.h
+# ---------------------------------------------------------------------------------------------
+class spt_prim(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("refl", ctypes.c_int32),
+                ("geom", ctypes.c_double * 5), ("e", ctypes.c_double * 3),
+                ("c", ctypes.c_double * 3)]
+
+
+class spt_camera(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_double * 3), ("lower_left_corner", ctypes.c_double * 3),
+                ("horizontal", ctypes.c_double * 3), ("vertical", ctypes.c_double * 3)]
+
+
+class spt_params(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("seed", ctypes.c_uint32), ("nee_prob", ctypes.c_float),
+                ("rr_depth", ctypes.c_int32), ("max_depth", ctypes.c_int32),
+                ("light_id", ctypes.c_int32),
+                ("light_x0", ctypes.c_float), ("light_dx", ctypes.c_float),
+                ("light_z0", ctypes.c_float), ("light_dz", ctypes.c_float),
+                ("light_y", ctypes.c_float), ("light_area", ctypes.c_float),
+                ("light_mode", ctypes.c_int32),
+                ("tile_rows", ctypes.c_int32), ("shard_index", ctypes.c_int32),
+                ("shard_count", ctypes.c_int32), ("chunk", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class spt_stats(ctypes.Structure):
+    _fields_ = [("samples", ctypes.c_uint64), ("path_rays", ctypes.c_uint64),
+                ("shadow_rays", ctypes.c_uint64), ("vertices", ctypes.c_uint64),
+                ("nee_events", ctypes.c_uint64), ("nee_light_hits", ctypes.c_uint64),
+                ("cosine_samples", ctypes.c_uint64), ("misses", ctypes.c_uint64),
+                ("flop", ctypes.c_double), ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+STAT_KEYS = ["samples", "path_rays", "shadow_rays", "vertices", "nee_events", "nee_light_hits",
+             "cosine_samples", "misses"]
+
+# Every entry point declared in include/spt.h (checked by tests/test_capi.py).
+EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_scene_spheres32",
+           "spt_shard_rows", "spt_render", "spt_context_create", "spt_context_destroy",
+           "spt_context_reserve", "spt_render_async", "spt_context_stats", "spt_abi_version",
+           "spt_status_string", "spt_last_error", "spt_device_count"]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libspt.so (built by __graft_entry__.build()). Fails loudly if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SptError(2, f"{path} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    P, I32, U32 = ctypes.POINTER, ctypes.c_int32, ctypes.c_uint32
+    lib.spt_default_params.argtypes = [P(spt_params)]
+    lib.spt_camera_init.argtypes = [P(spt_camera), P(ctypes.c_double), P(ctypes.c_double),
+                                    P(ctypes.c_double), ctypes.c_float, ctypes.c_float]
+    lib.spt_scene_cornell.argtypes = [P(spt_prim), I32, P(I32)]
+    lib.spt_scene_spheres32.argtypes = [P(spt_prim), I32, P(I32)]
+    lib.spt_shard_rows.argtypes = [P(spt_params), P(I32), I32]
+    lib.spt_shard_rows.restype = I32
+    lib.spt_render.argtypes = [P(spt_prim), I32, P(spt_camera), P(spt_params),
+                               P(ctypes.c_float), P(spt_stats)]
+    lib.spt_context_create.argtypes = [I32, P(ctypes.c_void_p)]
+    lib.spt_context_destroy.argtypes = [ctypes.c_void_p]
+    lib.spt_context_reserve.argtypes = [ctypes.c_void_p, I32, P(spt_params)]
+    lib.spt_render_async.argtypes = [ctypes.c_void_p, P(spt_prim), I32, P(spt_camera),
+                                     P(spt_params), ctypes.c_void_p, ctypes.c_void_p]
+    lib.spt_context_stats.argtypes = [ctypes.c_void_p, P(spt_stats)]
+    lib.spt_abi_version.restype = I32
+    lib.spt_status_string.argtypes = [I32]
+    lib.spt_status_string.restype = ctypes.c_char_p
+    lib.spt_last_error.restype = ctypes.c_char_p
+    lib.spt_device_count.restype = I32
+    for name in ("spt_default_params", "spt_camera_init", "spt_scene_cornell",
+                 "spt_scene_spheres32", "spt_render", "spt_context_create",
+                 "spt_context_destroy", "spt_context_reserve", "spt_render_async",
+                 "spt_context_stats"):
+        getattr(lib, name).restype = I32
+    del U32
+    _lib = lib
+    return lib
+
+
+def _check(status: int) -> None:
+    if status != 0:
+        msg = (load_library().spt_last_error() or b"").decode(errors="replace")
+        raise SptError(status, msg)
+
+
+# ---------------------------------------------------------------------------------------------
+# Reference-shaped host API
+# ---------------------------------------------------------------------------------------------
+def _v3(v) -> tuple:
+    if isinstance(v, (int, float)):
+        return (float(v), 0.0, 0.0)
+    t = tuple(float(x) for x in v)
+    return t + (0.0,) * (3 - len(t))
+
+
+class Vec(tuple):
+    """Vec :24-62 (only what scene construction needs: Vec(x=0, y=0, z=0), * scalar)."""
+
+    def __new__(cls, x=0.0, y=0.0, z=0.0):
+        return super().__new__(cls, (float(x), float(y), float(z)))
+
+    def __mul__(self, b):
+        return Vec(self[0] * b, self[1] * b, self[2] * b)
+
+    __rmul__ = __mul__
+
+
+def _prim(kind, geom, e, c, refl) -> spt_prim:
+    p = spt_prim()
+    p.kind, p.refl = kind, int(refl)
+    for i, g in enumerate(geom):
+        p.geom[i] = float(g)
+    for i, x in enumerate(_v3(e)):
+        p.e[i] = x
+    for i, x in enumerate(_v3(c)):
+        p.c[i] = x
+    return p
+
+
+def Rectangle_xz(x1, x2, z1, z2, y, e, c, refl=DIFF) -> spt_prim:  # :97-98
+    return _prim(RECT_XZ, (x1, x2, z1, z2, y), e, c, refl)
+
+
+def Rectangle_xy(x1, x2, y1, y2, z, e, c, refl=DIFF) -> spt_prim:  # :142
+    return _prim(RECT_XY, (x1, x2, y1, y2, z), e, c, refl)
+
+
+def Rectangle_yz(y1, y2, z1, z2, x, e, c, refl=DIFF) -> spt_prim:  # :185
+    return _prim(RECT_YZ, (y1, y2, z1, z2, x), e, c, refl)
+
+
+def Sphere(rad, p, e, c, refl=DIFF) -> spt_prim:  # :228
+    pp = _v3(p)
+    return _prim(SPHERE, (rad, pp[0], pp[1], pp[2], 0.0), e, c, refl)
+
+
+LOOKFROM = Vec(50, 40, 168)  # :65
+
+
+class Camera:
+    """Camera :256-285: Camera(lookfrom, lookat, vup, vfov, aspect); get_ray(s, t)."""
+
+    def __init__(self, lookfrom=LOOKFROM, lookat=(50, 40, 5), vup=(0, 1, 0), vfov=65.0,
+                 aspect=1.0):
+        lib = load_library()
+        self._c = spt_camera()
+        arr = lambda v: (ctypes.c_double * 3)(*_v3(v))  # noqa: E731
+        _check(lib.spt_camera_init(ctypes.byref(self._c), arr(lookfrom), arr(lookat), arr(vup),
+                                   float(vfov), float(aspect)))
+
+    @property
+    def origin(self):
+        return tuple(self._c.origin)
+
+    @property
+    def lower_left_corner(self):
+        return tuple(self._c.lower_left_corner)
+
+    @property
+    def horizontal(self):
+        return tuple(self._c.horizontal)
+
+    @property
+    def vertical(self):
+        return tuple(self._c.vertical)
+
+    def get_ray(self, s: float, t: float):  # :276-279
+        o, l, h, v = self.origin, self.lower_left_corner, self.horizontal, self.vertical
+        return o, tuple(l[i] + h[i] * s + v[i] * t - o[i] for i in range(3))
+
+
+def cornell_scene() -> list:
+    """rect[] of :287-311 via the library's builder (17 primitives)."""
+    lib = load_library()
+    arr = (spt_prim * 64)()
+    n = ctypes.c_int32()
+    _check(lib.spt_scene_cornell(arr, 64, ctypes.byref(n)))
+    return [arr[i] for i in range(n.value)]
+
+
+def spheres32_scene() -> list:
+    lib = load_library()
+    arr = (spt_prim * 64)()
+    n = ctypes.c_int32()
+    _check(lib.spt_scene_spheres32(arr, 64, ctypes.byref(n)))
+    return [arr[i] for i in range(n.value)]
+
+
+def default_params(**kw) -> spt_params:
+    p = spt_params()
+    _check(load_library().spt_default_params(ctypes.byref(p)))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown spt_params field {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+def shard_rows(params: spt_params) -> np.ndarray:
+    lib = load_library()
+    n = lib.spt_shard_rows(ctypes.byref(params), None, 0)
+    rows = (ctypes.c_int32 * max(n, 1))()
+    lib.spt_shard_rows(ctypes.byref(params), rows, n)
+    return np.frombuffer(rows, dtype=np.int32, count=n).copy()
+
+
+def _scene_array(prims: Sequence[spt_prim]):
+    arr = (spt_prim * len(prims))()
+    for i, p in enumerate(prims):
+        arr[i] = p
+    return arr
+
+
+def render(prims: Sequence[spt_prim], cam: Camera, params: spt_params, return_stats=False):
+    """Drop-in for :528-542: returns (rows, w, 3) float32 linear clamped RGB (rows = this shard's
+    rows, the whole image when shard_count == 1), y=0 top row. Runs on the GPU only."""
+    lib = load_library()
+    rows = int(lib.spt_shard_rows(ctypes.byref(params), None, 0))
+    out = np.empty((rows, params.width, 3), dtype=np.float32)
+    st = spt_stats()
+    _check(lib.spt_render(_scene_array(prims), len(prims), ctypes.byref(cam._c),
+                          ctypes.byref(params),
+                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(st)))
+    return (out, st.as_dict()) if return_stats else out
+
+
+class Renderer:
+    """Persistent device context for repeated renders into device buffers (torch tensors or raw
+    pointers) on a given HIP stream — what bench.py and the multi-GPU path use."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self._ctx = ctypes.c_void_p()
+        _check(self.lib.spt_context_create(int(device), ctypes.byref(self._ctx)))
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self.lib.spt_context_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    __del__ = close
+
+    def reserve(self, n_prims: int, params: spt_params):
+        _check(self.lib.spt_context_reserve(self._ctx, int(n_prims), ctypes.byref(params)))
+
+    def render_async(self, prims, cam: Camera, params: spt_params, rgb_dev_ptr: int,
+                     stream_ptr: int = 0):
+        self._prims = _scene_array(prims)
+        _check(self.lib.spt_render_async(self._ctx, self._prims, len(prims), ctypes.byref(cam._c),
+                                         ctypes.byref(params), ctypes.c_void_p(rgb_dev_ptr),
+                                         ctypes.c_void_p(stream_ptr)))
+
+    def stats(self) -> dict:
+        st = spt_stats()
+        _check(self.lib.spt_context_stats(self._ctx, ctypes.byref(st)))
+        return st.as_dict()
+
+
+# ---------------------------------------------------------------------------------------------
+# Output (:313-321, :548-551)
+# ---------------------------------------------------------------------------------------------
+def clamp(x):
+    return np.clip(x, 0.0, 1.0)
+
+
+def toInt(x) -> np.ndarray:
+    """int(pow(clamp(x), 1/2.2)*255 + .5) in double, as :319-321."""
+    x = np.asarray(x, dtype=np.float64)
+    return (np.power(np.clip(x, 0.0, 1.0), 1 / 2.2) * 255 + 0.5).astype(np.int64)
+
+
+def ppm_bytes(rgb: np.ndarray) -> bytes:
+    """ASCII P3 exactly as :549-551: header then '%d %d %d ' per pixel, no newlines."""
+    h, w, _ = rgb.shape
+    vals = toInt(rgb.reshape(-1, 3))
+    body = " ".join(f"{a} {b} {c}" for a, b, c in vals.tolist())
+    return (f"P3\n{w} {h}\n255\n" + body + (" " if len(vals) else "")).encode()
+
+
+def write_ppm(path: str, rgb: np.ndarray) -> None:
+    with open(path, "wb") as f:
+        f.write(ppm_bytes(rgb))
+
+
+def flop_model(stats: dict, prims: Iterable[spt_prim]) -> float:
+    """include/spt_flops.h model (same as the C side)."""
+    scene = sum(19 if p.kind == SPHERE else 6 for p in prims)
+    return (stats["samples"] * 40 + (stats["path_rays"] + stats["shadow_rays"]) * scene
+            + stats["vertices"] * 11 + (stats["vertices"] - stats["samples"]) * 12
+            + stats["cosine_samples"] * 65 + stats["nee_events"] * 19
+            + stats["nee_light_hits"] * 14)
+
+
+__all__ = [n for n in dir() if not n.startswith("_")]

@@ -1,0 +1,50 @@
+// smallpt_main.cpp — the reference's main() (smallpt.cpp:502-557) on the MI355X:
+//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--device N]
+// Same scene, camera (:521), clamp/toInt and P3 output; the pixel loop is one spt_render() call.
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+
+#include "smallpt.hpp"
+
+using namespace smallpt_amd;
+
+int main(int argc, char* argv[]) {
+  int pos[4] = {512, 512, 16, 1};  // :507-508 defaults, seed 1
+  const char* out = "image.ppm";
+  bool cosine = false;
+  int device = 0, npos = 0;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--cos")) cosine = true;
+    else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+    else if (npos < 4) pos[npos++] = std::atoi(argv[i]);
+    else out = argv[i];
+  }
+  const auto t1 = std::chrono::high_resolution_clock::now();
+  spt_params p;
+  spt_default_params(&p);
+  p.width = pos[0]; p.height = pos[1]; p.spp = pos[2]; p.seed = (uint32_t)pos[3];
+  p.nee_prob = cosine ? 0.0f : 1.0f;  // :464
+  p.device = device;
+  Camera cam(LOOKFROM, Vec(50, 40, 5), Vec(0, 1, 0), 65, float(p.width) / float(p.height));  // :521
+  spt_stats st{};
+  std::vector<float> c;
+  try {
+    c = render(cornell_scene(), cam, p, &st);
+  } catch (const std::exception& e) {
+    std::cerr << "render failed: " << e.what() << std::endl;
+    return 1;
+  }
+  if (write_ppm(out, p.width, p.height, c.data())) {
+    std::cerr << "cannot write " << out << std::endl;
+    return 1;
+  }
+  const auto t2 = std::chrono::high_resolution_clock::now();
+  const double samples = (double)p.width * p.height * p.spp;
+  std::cout << "KERNEL_MS : " << st.kernel_ms << "  MSAMPLES/S : " << samples / (st.kernel_ms * 1e3)
+            << "  VERTICES/SAMPLE : " << (double)st.vertices / samples << std::endl;
+  std::cout << " DURATION : " << std::chrono::duration_cast<std::chrono::milliseconds>(t2 - t1).count()
+            << std::endl;  // :554-556
+  return 0;
+}

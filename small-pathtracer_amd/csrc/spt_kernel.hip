@@ -1,0 +1,637 @@
+// spt_kernel.hip — MI355X (gfx950) render kernel for the smallpt per-pixel sampling loop,
+// and the C ABI of include/spt.h.
+//
+// Replaces /root/reference/src/smallpt.cpp:528-542 (pixel x sample loop) and :419-480
+// (recursive radiance()) with one persistent-lane kernel:
+//   * one lane = one pixel-sample path at a time; radiance()'s recursion is an iterative bounce
+//     loop in registers (T = throughput, L = radiance so far);
+//   * work units = (pixel, chunk of samples); a wave pulls units from a global atomic queue and
+//     hands them to its idle lanes with a ballot + mbcnt prefix sum, so lanes whose paths end by
+//     Russian roulette / light hits immediately start the next sample (no idle SIMD slots until
+//     the queue drains);
+//   * the scene (<= 64 primitives) is read with wave-uniform scalar loads in the intersect loop
+//     (intersect() :323-335 is a broadcast, never a per-lane HBM read) and staged into LDS for
+//     the per-lane (divergent) lookups of the hit primitive;
+//   * Philox4x32-10 counter RNG keyed by (seed; pixel, sample, vertex, stream);
+//   * per-pixel accumulation in 32.32 fixed point with 64-bit integer atomics: exact, independent
+//     of unit size, lane order, queue order and GPU count.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/spt.h"
+#include "../../include/spt_flops.h"
+#include "spt_device.h"
+
+namespace spt {
+
+constexpr int kMaxPrims = 64;
+constexpr int kBlock = 256;
+constexpr uint32_t kGrab = 64;  // units fetched per queue atomic
+
+// 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
+// axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
+struct alignas(16) DevPrim {
+  int kind;
+  float w1, w2, w3, w4, w5, pad0, pad1;
+  float ex, ey, ez, pmax;
+  float cx, cy, cz, pad2;
+};
+static_assert(sizeof(DevPrim) == 64, "DevPrim layout");
+
+struct KParams {
+  const DevPrim* prims;
+  int n_prims;
+  float cam[12];  // origin, lower_left_corner, horizontal, vertical
+  int width, height, spp;
+  uint32_t key0, key1;
+  float nee_prob;
+  int rr_depth, max_depth, light_id;
+  float lx0, ldx, lz0, ldz, ly, larea;
+  int light_mode;
+  uint32_t ldxi, ldzi;
+  int tile_rows, shard_index, shard_count;
+  int chunk, n_local_pix;
+  uint32_t n_units;
+  float inv_spp;
+  unsigned long long* accum;  // [n_local_pix][3] 32.32 fixed point
+  uint32_t* queue;            // [0] = next unit
+  unsigned long long* stats;  // [8]
+};
+
+// Scene intersection of the counter-mode contract (intersect :323-335 over Rectangle_* :102-112 /
+// Sphere :229-239). Uniform loop over primitives: every read of P.prims[i] is wave-uniform and
+// becomes a scalar (s_load) broadcast. Ties keep the lowest index; id untouched on a miss.
+__device__ __forceinline__ bool intersect_scene(const KParams& P, f3 o, f3 d, float& t_out,
+                                                int& id) {
+  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  float tmin = 1e20f;
+  const DevPrim* __restrict__ S = P.prims;
+  for (int i = 0; i < P.n_prims; ++i) {
+    const int kind = S[i].kind;
+    float tt, a, b;
+    if (kind == SPT_RECT_XY) {
+      tt = (S[i].w1 - o.z) * iz; a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y);
+    } else if (kind == SPT_RECT_XZ) {
+      tt = (S[i].w1 - o.y) * iy; a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z);
+    } else if (kind == SPT_RECT_YZ) {
+      tt = (S[i].w1 - o.x) * ix; a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z);
+    } else {  // sphere, det = r^2 - |op - b d|^2
+      const f3 op = mk(S[i].w1 - o.x, S[i].w2 - o.y, S[i].w3 - o.z);
+      const float bb = dot3(op, d);
+      const f3 q = mk(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+      const float det = S[i].w4 - dot3(q, q);
+      if (det >= 0.0f) {
+        const float sd = sqrtf(det);
+        const float t1 = bb - sd, t2 = bb + sd;
+        const float ts = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+        if (ts != 0.0f && ts < tmin) { tmin = ts; id = i; }
+      }
+      continue;
+    }
+    const bool acc = (a >= S[i].w2) & (a <= S[i].w3) & (b >= S[i].w4) & (b <= S[i].w5) &
+                     (tt > 0.0f) & (tt < tmin);
+    tmin = acc ? tt : tmin;
+    id = acc ? i : id;
+  }
+  t_out = tmin;
+  return tmin < 1e20f;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
+  __shared__ DevPrim s_prims[kMaxPrims];
+  for (int i = threadIdx.x; i < P.n_prims; i += kBlock) s_prims[i] = P.prims[i];
+  __syncthreads();
+
+  const uint32_t lane = __lane_id();
+  // ---- per-lane state
+  bool has_unit = false, need_cam = true, carried = false, c_hit = false;
+  uint32_t lp = 0, s = 0, s_end = 0, pix = 0;
+  int px = 0, py = 0, depth = 0, c_id = 0;
+  float c_t = 0.0f;
+  unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
+  f3 o = mk(0, 0, 0), d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0);
+  // ---- wave-uniform state
+  uint32_t pool_next = 0, pool_end = 0;
+  bool exhausted = false;
+  uint32_t n_samples = 0, n_path = 0, n_shadow = 0, n_vert = 0, n_nee = 0, n_nee_hit = 0,
+           n_cos = 0, n_miss = 0;
+
+  for (;;) {
+    // 1) retire finished units: flush the fixed-point sums of their pixel.
+    if (has_unit && need_cam && s >= s_end) {
+      unsigned long long* a = P.accum + 3ull * lp;
+      if (acc0) atomicAdd(a + 0, acc0);
+      if (acc1) atomicAdd(a + 1, acc1);
+      if (acc2) atomicAdd(a + 2, acc2);
+      acc0 = acc1 = acc2 = 0;
+      has_unit = false;
+    }
+    // 2) refill idle lanes from the wave's pool (ballot + mbcnt prefix sum), pool from the queue.
+    bool needs_unit = !has_unit;
+    uint64_t need = __ballot(needs_unit);
+    while (need != 0 && !exhausted) {
+      if (pool_next >= pool_end) {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(P.queue, kGrab);
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (b >= P.n_units) { exhausted = true; break; }
+        pool_next = b;
+        pool_end = min(b + kGrab, P.n_units);
+      }
+      const uint32_t rank = lane_rank(need);
+      const uint32_t avail = pool_end - pool_next;
+      if (needs_unit && rank < avail) {
+        const uint32_t u = pool_next + rank;
+        const uint32_t j = u / (uint32_t)P.n_local_pix;  // chunk-major: lanes get adjacent pixels
+        lp = u - j * (uint32_t)P.n_local_pix;
+        s = j * (uint32_t)P.chunk;
+        s_end = min(s + (uint32_t)P.chunk, (uint32_t)P.spp);
+        const uint32_t lr = lp / (uint32_t)P.width;
+        px = (int)(lp - lr * (uint32_t)P.width);
+        const uint32_t tile = lr / (uint32_t)P.tile_rows, within = lr - tile * (uint32_t)P.tile_rows;
+        py = (int)((tile * (uint32_t)P.shard_count + (uint32_t)P.shard_index) *
+                       (uint32_t)P.tile_rows + within);
+        pix = (uint32_t)py * (uint32_t)P.width + (uint32_t)px;
+        has_unit = true;
+        needs_unit = false;
+        need_cam = true;
+      }
+      pool_next += min((uint32_t)__popcll(need), avail);
+      need = __ballot(needs_unit);
+    }
+    if (__ballot(has_unit) == 0) break;
+
+    // per-lane events of this iteration, counted by ballots at the convergent end of the loop
+    bool ev_cam = false, ev_path = false, ev_miss = false, ev_vert2 = false, ev_nee = false,
+         ev_nee_hit = false, ev_cos = false;
+    const bool ev_vert = has_unit;
+    if (has_unit) {
+      // 3) camera ray for lanes starting a sample (:533-536).
+      if (need_cam) {
+        const u4 r = philox4x32_10(pix, s, 0u, 0u, P.key0, P.key1);
+        const float su = (((float)px - 0.5f) + u01(r.x)) / (float)P.width;
+        const float sv = (((float)(P.height - py - 1) - 0.5f) + u01(r.y)) / (float)P.height;
+        o = mk(P.cam[0], P.cam[1], P.cam[2]);
+        d = normalize3(mk(fmaf(P.cam[9], sv, fmaf(P.cam[6], su, P.cam[3])) - P.cam[0],
+                          fmaf(P.cam[10], sv, fmaf(P.cam[7], su, P.cam[4])) - P.cam[1],
+                          fmaf(P.cam[11], sv, fmaf(P.cam[8], su, P.cam[5])) - P.cam[2]));
+        T = mk(1, 1, 1);
+        L = mk(0, 0, 0);
+        depth = 0;
+        carried = false;
+        need_cam = false;
+        ev_cam = true;
+      }
+      // 4) vertex: hittingPoint :371-377 (or the hit carried from a NEE shadow ray).
+      int id = 0;
+      float t;
+      bool hit;
+      if (carried) {
+        hit = c_hit; t = c_t; id = hit ? c_id : 0;
+        carried = false;
+      } else {
+        hit = intersect_scene(P, o, d, t, id);
+        ev_path = true;
+      }
+      const DevPrim& H = s_prims[id];
+      const int kind = H.kind;
+      f3 x;
+      if (!hit) {
+        x = mk(0, 0, 0);
+        ev_miss = true;
+      } else {
+        float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
+        if (kind == SPT_RECT_XY) tr = (H.w1 - o.z) / d.z;
+        else if (kind == SPT_RECT_XZ) tr = (H.w1 - o.y) / d.y;
+        else if (kind == SPT_RECT_YZ) tr = (H.w1 - o.x) / d.x;
+        x = mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
+      }
+      f3 nl;  // Hitable::normal, oriented against the ray (:123,:166,:209,:251)
+      if (kind == SPT_RECT_XY) nl = d.z < 0.0f ? mk(0, 0, 1) : mk(0, 0, -1);
+      else if (kind == SPT_RECT_XZ) nl = d.y < 0.0f ? mk(0, 1, 0) : mk(0, -1, 0);
+      else if (kind == SPT_RECT_YZ) nl = d.x < 0.0f ? mk(1, 0, 0) : mk(-1, 0, 0);
+      else {
+        const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
+        nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
+      }
+      f3 f = mk(H.cx, H.cy, H.cz);
+      const f3 e = mk(H.ex, H.ey, H.ez);
+      const float p = H.pmax;
+      ++depth;
+      // Russian roulette :448-454 (+ optional hard depth cap).
+      bool term = false;
+      if (P.max_depth > 0 && depth >= P.max_depth) {
+        term = true;
+      } else if (depth > P.rr_depth || p == 0.0f) {
+        if (!(p > 0.0f)) {
+          term = true;
+        } else {
+          bool keep = true;
+          if (p < 1.0f) {
+            const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, P.key0, P.key1);
+            keep = u01(r.x) < p;
+          }
+          if (keep) {
+            const float ip = 1.0f / p;
+            f = mk(f.x * ip, f.y * ip, f.z * ip);
+          } else {
+            term = true;
+          }
+        }
+      }
+      if (!term) {
+        // DIFF :457-480.
+        bool nee;
+        if (P.nee_prob >= 1.0f) nee = true;
+        else if (P.nee_prob <= 0.0f) nee = false;
+        else {
+          const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, P.key0, P.key1);
+          nee = u01(r.y) < P.nee_prob;
+        }
+        const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 0u, P.key0, P.key1);
+        float w = 1.0f;
+        f3 dn;
+        bool light_end = false;
+        f3 e_light = mk(0, 0, 0);
+        bool scatter = true;
+        if (nee) {
+          // light_sampling :363-369, shadow ray :466, NEE weight :471-472.
+          float xl, zl;
+          if (P.light_mode == SPT_LIGHT_GLIBC_WRAP) {
+            xl = fmaf((float)(int32_t)((r.x >> 1) * P.ldxi), 0x1p-31f, P.lx0);
+            zl = fmaf((float)(int32_t)((r.y >> 1) * P.ldzi), 0x1p-31f, P.lz0);
+          } else {
+            xl = fmaf(u01(r.x), P.ldx, P.lx0);
+            zl = fmaf(u01(r.y), P.ldz, P.lz0);
+          }
+          const f3 dl = normalize3(mk(xl - x.x, P.ly - x.y, zl - x.z));
+          int ids = id;
+          float ts;
+          const bool sh = intersect_scene(P, x, dl, ts, ids);
+          ev_nee = true;
+          if (ids == P.light_id) {
+            ev_nee_hit = true;
+            const float pdf = fabsf((P.larea * dl.y) / (ts * ts));
+            const float brdf = fabsf(dot3(dl, nl) * 0.318309886183790672f);
+            w = pdf * brdf;
+            dn = dl;
+            scatter = false;
+            if (sh && s_prims[ids].pmax == 0.0f) {
+              // The next vertex is the (black) light hit by this very ray: RR with p == 0 ends
+              // the path there (:448-453) returning its emission — finish it inline.
+              light_end = true;
+              e_light = mk(s_prims[ids].ex, s_prims[ids].ey, s_prims[ids].ez);
+            } else {
+              carried = true; c_hit = sh; c_t = ts; c_id = ids;
+            }
+          }
+        }
+        if (scatter) {
+          dn = cosine_dir(nl, r.z, r.w);
+          ev_cos = true;
+        }
+        L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+        T = mk((T.x * f.x) * w, (T.y * f.y) * w, (T.z * f.z) * w);
+        o = x;
+        d = dn;
+        if (light_end) {
+          ev_vert2 = true;
+          L = mk(fmaf(T.x, e_light.x, L.x), fmaf(T.y, e_light.y, L.y), fmaf(T.z, e_light.z, L.z));
+          term = true;
+        }
+      } else {
+        L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+      }
+      if (term) {
+        acc0 += fix32(L.x, P.inv_spp);
+        acc1 += fix32(L.y, P.inv_spp);
+        acc2 += fix32(L.z, P.inv_spp);
+        ++s;
+        need_cam = true;
+      }
+    }
+    n_samples += (uint32_t)__popcll(__ballot(ev_cam));
+    n_path += (uint32_t)__popcll(__ballot(ev_path));
+    n_miss += (uint32_t)__popcll(__ballot(ev_miss));
+    n_vert += (uint32_t)__popcll(__ballot(ev_vert)) + (uint32_t)__popcll(__ballot(ev_vert2));
+    n_nee += (uint32_t)__popcll(__ballot(ev_nee));
+    n_shadow += (uint32_t)__popcll(__ballot(ev_nee));
+    n_nee_hit += (uint32_t)__popcll(__ballot(ev_nee_hit));
+    n_cos += (uint32_t)__popcll(__ballot(ev_cos));
+  }
+  if (lane == 0) {
+    atomicAdd(P.stats + 0, (unsigned long long)n_samples);
+    atomicAdd(P.stats + 1, (unsigned long long)n_path);
+    atomicAdd(P.stats + 2, (unsigned long long)n_shadow);
+    atomicAdd(P.stats + 3, (unsigned long long)n_vert);
+    atomicAdd(P.stats + 4, (unsigned long long)n_nee);
+    atomicAdd(P.stats + 5, (unsigned long long)n_nee_hit);
+    atomicAdd(P.stats + 6, (unsigned long long)n_cos);
+    atomicAdd(P.stats + 7, (unsigned long long)n_miss);
+  }
+}
+
+// 32.32 fixed point -> float, clamp :538 (values are >= 0 by construction).
+__global__ void __launch_bounds__(kBlock)
+finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict__ rgb, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) {
+    const float v = (float)accum[i] * 0x1p-32f;
+    rgb[i] = v > 1.0f ? 1.0f : v;
+  }
+}
+
+}  // namespace spt
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+using namespace spt;
+
+static thread_local std::string g_last_error;
+static spt_status fail(spt_status s, const std::string& msg) {
+  g_last_error = msg;
+  return s;
+}
+#define SPT_HIP(call)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(e_ == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP,                 \
+                  std::string(#call) + ": " + hipGetErrorString(e_));                    \
+  } while (0)
+
+struct spt_context {
+  int device = 0;
+  int n_cu = 0, blocks_per_cu = 0;
+  DevPrim* prims = nullptr;
+  unsigned long long* accum = nullptr;
+  size_t accum_cap = 0;  // elements
+  uint32_t* queue = nullptr;
+  unsigned long long* stats = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool pending = false;
+  int n_prims = 0;
+  KParams last{};
+};
+
+extern "C" int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
+int spt_shard_row_count(const spt_params* p);  // spt_host.cpp
+
+static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* cam,
+                           const spt_params* p) {
+  if (!prims || !cam || !p) return fail(SPT_ERR_INVALID_ARG, "null argument");
+  if (n <= 0 || n > kMaxPrims) return fail(SPT_ERR_INVALID_ARG, "n_prims must be in [1, 64]");
+  if (p->width <= 0 || p->height <= 0 || p->spp <= 0)
+    return fail(SPT_ERR_INVALID_ARG, "width/height/spp must be positive");
+  if ((uint64_t)p->width * (uint64_t)p->height > 0xFFFFFFFFull)
+    return fail(SPT_ERR_INVALID_ARG, "image too large for 32-bit pixel counters");
+  if (p->shard_count < 1 || p->shard_index < 0 || p->shard_index >= p->shard_count)
+    return fail(SPT_ERR_INVALID_ARG, "bad shard_index/shard_count");
+  if (p->tile_rows < 0 || p->chunk < 0) return fail(SPT_ERR_INVALID_ARG, "negative tile/chunk");
+  if (p->flags != 0) return fail(SPT_ERR_INVALID_ARG, "flags must be 0");
+  if (p->light_mode != SPT_LIGHT_GLIBC_WRAP && p->light_mode != SPT_LIGHT_UNIFORM)
+    return fail(SPT_ERR_INVALID_ARG, "bad light_mode");
+  if (p->light_mode == SPT_LIGHT_GLIBC_WRAP &&
+      (p->light_dx != (float)(uint32_t)p->light_dx || p->light_dz != (float)(uint32_t)p->light_dz))
+    return fail(SPT_ERR_INVALID_ARG, "GLIBC_WRAP light sampling needs integral light_dx/dz");
+  for (int i = 0; i < n; ++i) {
+    if (prims[i].kind < SPT_RECT_XY || prims[i].kind > SPT_SPHERE)
+      return fail(SPT_ERR_INVALID_ARG, "bad primitive kind");
+    if (prims[i].refl != SPT_DIFF)
+      return fail(SPT_ERR_UNSUPPORTED, "only DIFF materials are live in the reference (:457)");
+  }
+  return SPT_OK;
+}
+
+static void to_dev(const spt_prim* s, int n, DevPrim* out) {
+  for (int i = 0; i < n; ++i) {
+    DevPrim P;
+    std::memset(&P, 0, sizeof P);
+    P.kind = s[i].kind;
+    if (s[i].kind == SPT_SPHERE) {
+      const float r = (float)s[i].geom[0];
+      P.w1 = (float)s[i].geom[1]; P.w2 = (float)s[i].geom[2]; P.w3 = (float)s[i].geom[3];
+      P.w4 = r * r;
+    } else {
+      P.w1 = (float)s[i].geom[4];
+      P.w2 = (float)s[i].geom[0]; P.w3 = (float)s[i].geom[1];
+      P.w4 = (float)s[i].geom[2]; P.w5 = (float)s[i].geom[3];
+    }
+    P.ex = (float)s[i].e[0]; P.ey = (float)s[i].e[1]; P.ez = (float)s[i].e[2];
+    P.cx = (float)s[i].c[0]; P.cy = (float)s[i].c[1]; P.cz = (float)s[i].c[2];
+    P.pmax = P.cx > P.cy && P.cx > P.cz ? P.cx : P.cy > P.cz ? P.cy : P.cz;  // :447
+    out[i] = P;
+  }
+}
+
+static int tile_rows_of(const spt_params* p) { return p->tile_rows > 0 ? p->tile_rows : 8; }
+
+extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
+  if (!out) return fail(SPT_ERR_INVALID_ARG, "null out");
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+    return fail(SPT_ERR_NO_DEVICE, "no HIP device");
+  if (device < 0 || device >= count) return fail(SPT_ERR_INVALID_ARG, "bad device ordinal");
+  SPT_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  SPT_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(SPT_ERR_NO_DEVICE, std::string("built for gfx950, device is ") + prop.gcnArchName);
+  spt_context* c = new spt_context();
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount;
+  int bpc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel, kBlock, 0) != hipSuccess ||
+      bpc <= 0)
+    bpc = 4;
+  c->blocks_per_cu = bpc;
+  hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
+  if (e == hipSuccess) e = hipMalloc(&c->queue, sizeof(uint32_t) * 64);
+  if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * 8);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e != hipSuccess) {
+    spt_context_destroy(c);
+    return fail(SPT_ERR_OOM, std::string("context alloc: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return SPT_OK;
+}
+
+extern "C" spt_status spt_context_destroy(spt_context* c) {
+  if (!c) return SPT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->prims) (void)hipFree(c->prims);
+  if (c->accum) (void)hipFree(c->accum);
+  if (c->queue) (void)hipFree(c->queue);
+  if (c->stats) (void)hipFree(c->stats);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+  return SPT_OK;
+}
+
+extern "C" spt_status spt_context_reserve(spt_context* c, int32_t n_prims, const spt_params* p) {
+  if (!c || !p) return fail(SPT_ERR_INVALID_ARG, "null argument");
+  (void)n_prims;
+  const size_t need = 3ull * (size_t)spt_shard_row_count(p) * (size_t)p->width;
+  if (need > c->accum_cap) {
+    SPT_HIP(hipSetDevice(c->device));
+    if (c->accum) SPT_HIP(hipFree(c->accum));
+    c->accum = nullptr;
+    c->accum_cap = 0;
+    SPT_HIP(hipMalloc(&c->accum, need * sizeof(unsigned long long)));
+    c->accum_cap = need;
+  }
+  return SPT_OK;
+}
+
+extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, int32_t n_prims,
+                                       const spt_camera* cam, const spt_params* p, float* rgb_dev,
+                                       void* stream_v) {
+  if (!c || !rgb_dev) return fail(SPT_ERR_INVALID_ARG, "null context/output");
+  spt_status st = validate(prims, n_prims, cam, p);
+  if (st != SPT_OK) return st;
+  st = spt_context_reserve(c, n_prims, p);
+  if (st != SPT_OK) return st;
+  SPT_HIP(hipSetDevice(c->device));
+  hipStream_t stream = (hipStream_t)stream_v;
+
+  KParams K{};
+  DevPrim host_prims[kMaxPrims];
+  to_dev(prims, n_prims, host_prims);
+  SPT_HIP(hipMemcpyAsync(c->prims, host_prims, sizeof(DevPrim) * n_prims, hipMemcpyHostToDevice,
+                         stream));
+  K.prims = c->prims;
+  K.n_prims = n_prims;
+  for (int i = 0; i < 3; ++i) {
+    K.cam[i] = (float)cam->origin[i];
+    K.cam[3 + i] = (float)cam->lower_left_corner[i];
+    K.cam[6 + i] = (float)cam->horizontal[i];
+    K.cam[9 + i] = (float)cam->vertical[i];
+  }
+  K.width = p->width; K.height = p->height; K.spp = p->spp;
+  K.key0 = p->seed; K.key1 = SPT_PHILOX_KEY1;
+  K.nee_prob = p->nee_prob; K.rr_depth = p->rr_depth; K.max_depth = p->max_depth;
+  K.light_id = p->light_id;
+  K.lx0 = p->light_x0; K.ldx = p->light_dx; K.lz0 = p->light_z0; K.ldz = p->light_dz;
+  K.ly = p->light_y; K.larea = p->light_area; K.light_mode = p->light_mode;
+  K.ldxi = p->light_mode == SPT_LIGHT_GLIBC_WRAP ? (uint32_t)p->light_dx : 0u;
+  K.ldzi = p->light_mode == SPT_LIGHT_GLIBC_WRAP ? (uint32_t)p->light_dz : 0u;
+  K.tile_rows = tile_rows_of(p); K.shard_index = p->shard_index; K.shard_count = p->shard_count;
+  const int rows = spt_shard_row_count(p);
+  K.n_local_pix = rows * p->width;
+  // Unit size: enough units for >= 8 per resident lane so the queue drains evenly; never
+  // changes results (integer accumulation).
+  int chunk = p->chunk;
+  if (chunk <= 0) {
+    const double lanes = (double)c->n_cu * c->blocks_per_cu * kBlock;
+    const double want_units = 8.0 * lanes;
+    const double per_pix = std::max(1.0, want_units / std::max(1, K.n_local_pix));
+    chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
+    chunk = std::min(chunk, p->spp);
+  }
+  K.chunk = chunk;
+  const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
+  const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
+  if (n_units >= 0xFFFF0000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
+  K.n_units = (uint32_t)n_units;
+  K.inv_spp = 1.0f / (float)p->spp;
+  K.accum = c->accum;
+  K.queue = c->queue;
+  K.stats = c->stats;
+  c->n_prims = n_prims;
+  c->last = K;
+
+  SPT_HIP(hipMemsetAsync(c->accum, 0, sizeof(unsigned long long) * 3 * (size_t)K.n_local_pix,
+                         stream));
+  SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream));
+  SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 8, stream));
+  const int grid = c->n_cu * c->blocks_per_cu;
+  SPT_HIP(hipEventRecord(c->ev0, stream));
+  hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), 0, stream, K);
+  SPT_HIP(hipGetLastError());
+  SPT_HIP(hipEventRecord(c->ev1, stream));
+  const uint32_t n = 3u * (uint32_t)K.n_local_pix;
+  hipLaunchKernelGGL(finalize_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                     (const unsigned long long*)c->accum, rgb_dev, n);
+  SPT_HIP(hipGetLastError());
+  c->pending = true;
+  return SPT_OK;
+}
+
+extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
+  if (!c || !out) return fail(SPT_ERR_INVALID_ARG, "null argument");
+  SPT_HIP(hipSetDevice(c->device));
+  SPT_HIP(hipEventSynchronize(c->ev1));
+  unsigned long long h[8];
+  SPT_HIP(hipMemcpy(h, c->stats, sizeof h, hipMemcpyDeviceToHost));
+  float ms = 0.0f;
+  SPT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  std::memset(out, 0, sizeof *out);
+  out->samples = h[0]; out->path_rays = h[1]; out->shadow_rays = h[2]; out->vertices = h[3];
+  out->nee_events = h[4]; out->nee_light_hits = h[5]; out->cosine_samples = h[6];
+  out->misses = h[7];
+  // FLOP model (include/spt_flops.h): scene cost per ray from the primitive mix.
+  DevPrim hp[kMaxPrims];
+  SPT_HIP(hipMemcpy(hp, c->prims, sizeof(DevPrim) * c->n_prims, hipMemcpyDeviceToHost));
+  double scene = 0;
+  for (int i = 0; i < c->n_prims; ++i) scene += hp[i].kind == SPT_SPHERE ? SPT_FLOP_SPHERE : SPT_FLOP_RECT;
+  out->flop = (double)out->samples * SPT_FLOP_SAMPLE +
+              (double)(out->path_rays + out->shadow_rays) * scene +
+              (double)out->vertices * SPT_FLOP_VERTEX +
+              (double)(out->vertices - out->samples) * SPT_FLOP_COMBINE +
+              (double)out->cosine_samples * SPT_FLOP_COSINE +
+              (double)out->nee_events * SPT_FLOP_NEE + (double)out->nee_light_hits * SPT_FLOP_NEE_HIT;
+  out->kernel_ms = ms;
+  c->pending = false;
+  return SPT_OK;
+}
+
+extern "C" spt_status spt_render(const spt_prim* prims, int32_t n_prims, const spt_camera* cam,
+                                 const spt_params* p, float* rgb_out, spt_stats* stats) {
+  if (!rgb_out) return fail(SPT_ERR_INVALID_ARG, "null rgb_out");
+  spt_status st = validate(prims, n_prims, cam, p);
+  if (st != SPT_OK) return st;
+  spt_context* c = nullptr;
+  st = spt_context_create(p->device, &c);
+  if (st != SPT_OK) return st;
+  const size_t n = 3ull * (size_t)spt_shard_row_count(p) * (size_t)p->width;
+  float* dev = nullptr;
+  hipError_t e = hipMalloc(&dev, n * sizeof(float));
+  if (e != hipSuccess) {
+    spt_context_destroy(c);
+    return fail(SPT_ERR_OOM, "output alloc");
+  }
+  st = spt_render_async(c, prims, n_prims, cam, p, dev, nullptr);
+  if (st == SPT_OK) {
+    spt_stats tmp;
+    st = spt_context_stats(c, stats ? stats : &tmp);
+  }
+  if (st == SPT_OK) {
+    e = hipMemcpy(rgb_out, dev, n * sizeof(float), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) st = fail(SPT_ERR_HIP, hipGetErrorString(e));
+  }
+  (void)hipFree(dev);
+  spt_context_destroy(c);
+  return st;
+}
+
+extern "C" int32_t spt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" const char* spt_last_error(void) { return g_last_error.c_str(); }

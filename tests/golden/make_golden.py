@@ -1,0 +1,84 @@
+"""Regenerate tests/golden/ from the reference itself (run in the dev container only).
+
+Builds oracle/_ref/smallpt_{nee,cos} from /root/reference/src/smallpt.cpp via oracle/build_ref.sh
+(the SURVEY.md Appendix A patch streamed through sed into g++ -O3; no reference source is copied),
+runs it, and stores:
+  ref_64x48_s4_{nee,cos}.ppm   the reference's own output PPMs (data fixtures)
+  golden.json                  md5s of the reference PPMs for 64x48@4 and 256x192@4 (NEE, cosine),
+                               the build recipe, known-answer values, and counter-mode md5s
+  counter_64x48_s16_{nee,cos}.npy  counter-mode contract images from oracle/ (regression pins for
+                               the GPU kernel; produced by the oracle, not by the reference)
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+
+def md5(path):
+    return hashlib.md5(open(path, "rb").read()).hexdigest()
+
+
+def main():
+    if not os.path.exists("/root/reference/src/smallpt.cpp"):
+        sys.exit("reference not present: golden fixtures can only be regenerated in the dev container")
+    subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
+    ref = os.path.join(ROOT, "oracle", "_ref")
+    out = {"recipe": "oracle/build_ref.sh: sed patch of smallpt.cpp (:424-442 deleted, srand(seed), "
+                     "argv w h spp seed out, :517 skipped; cosine: :464 q<1 -> q<0) | g++ -O3 (x86-64 "
+                     "baseline, g++ 11.4)", "reference_md5": {}}
+    tmp = "/tmp/spt_golden"
+    os.makedirs(tmp, exist_ok=True)
+    for w, h, spp in ((64, 48, 4), (256, 192, 4)):
+        for est in ("nee", "cos"):
+            path = os.path.join(tmp, f"ref_{w}x{h}_s{spp}_{est}.ppm")
+            subprocess.run([os.path.join(ref, f"smallpt_{est}"), str(w), str(h), str(spp), "1", path],
+                           check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            out["reference_md5"][f"{w}x{h}_s{spp}_seed1_{est}"] = md5(path)
+            if w == 64:
+                with open(path, "rb") as f, open(os.path.join(HERE, os.path.basename(path)), "wb") as g:
+                    g.write(f.read())
+    # Known answers (measured by calling the reference's own functions).
+    out["kat"] = {
+        "camera_aspect1": {"llc": [49.362929701805115, 39.362929701805115, 167],
+                           "horizontal": [1.2741405963897705, -0.0, 0], "vertical": [0, 1.2741405963897705, 0]},
+        "camera_aspect4_3": {"llc": [49.150572896003723, 39.362929701805115, 167],
+                             "horizontal": [1.6988542079925537, -0.0, 0], "vertical": [0, 1.2741405963897705, 0]},
+        "erand48_row_seeds": {"0": [3.907985046680551e-14, 0.00098539467465030839, 0.041631001594613082],
+                              "1": [0.90010070800785158, 0.041650067526212808, 0.81001784241492558],
+                              "3385": [0.84089660644535158, 0.65090299721371281, 0.031087178352425582],
+                              "2303": [0.93193054199222658, 0.65172697182308781, 0.63652541077430058]},
+        "glibc_srand1_first3": [1804289383, 846930886, 1681692777],
+        # Random123 kat_vectors, philox4x32 R=10
+        "philox4x32_10": [
+            {"ctr": [0, 0, 0, 0], "key": [0, 0], "out": [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]},
+            {"ctr": [0xffffffff] * 4, "key": [0xffffffff] * 2, "out": [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]},
+            {"ctr": [0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], "key": [0xa4093822, 0x299f31d0],
+             "out": [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]},
+        ],
+    }
+    # Counter-mode contract pins (oracle output) for the GPU regression tests.
+    from oracle import oracle as o
+    o.build()
+    prims = o.scene_cornell()
+    out["counter_md5"] = {}
+    for est, q in (("nee", 1.0), ("cos", 0.0)):
+        p = o.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q)
+        img, st = o.counter_render(prims, o.camera(64 / 48), p)
+        np.save(os.path.join(HERE, f"counter_64x48_s16_{est}.npy"), img)
+        out["counter_md5"][est] = hashlib.md5(img.tobytes()).hexdigest()
+        out.setdefault("counter_stats", {})[est] = st
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out["reference_md5"], indent=1))
+
+
+if __name__ == "__main__":
+    main()

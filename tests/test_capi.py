@@ -1,0 +1,108 @@
+"""The C ABI library loads, exports every symbol include/spt.h declares, and its host helpers match
+the reference's host API (restated independently by the oracle). No GPU compute here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "spt.h")).read()
+    return sorted(set(re.findall(r"\b(spt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol(spt):
+    declared = _declared_symbols()
+    assert sorted(spt.EXPORTS) == declared
+    out = subprocess.run(["nm", "-D", "--defined-only", spt.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (spt_\w+)", out))
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    lib = spt.load_library()
+    for s in declared:
+        assert getattr(lib, s) is not None
+
+
+def test_abi_version_and_status_strings(spt):
+    lib = spt.load_library()
+    assert lib.spt_abi_version() == 1
+    for code, text in spt.STATUS.items():
+        assert lib.spt_status_string(code).decode() == text
+
+
+def test_library_is_gfx950_code_object(spt):
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", spt.LIB_PATH], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("roc-obj-ls unavailable")
+    assert "gfx950" in out.stdout
+
+
+def test_scene_builder_matches_reference_scene(spt, oracle):
+    mine = spt.cornell_scene()
+    ref = oracle.scene_cornell()
+    assert len(mine) == len(ref) == 17
+    for a, b in zip(mine, ref):
+        assert bytes(a) == bytes(b)
+
+
+def test_python_ctor_mirror_matches(spt, oracle):
+    ref = oracle.scene_cornell()
+    assert bytes(spt.Rectangle_xy(1, 99, 0, 81.6, 0, spt.Vec(), spt.Vec(.75, .75, .75), spt.DIFF)) == bytes(ref[0])
+    assert bytes(spt.Rectangle_xz(32, 68, 63, 96, 81.5, spt.Vec(12, 12, 12), spt.Vec(), spt.DIFF)) == bytes(ref[6])
+    assert bytes(spt.Rectangle_yz(0, 25, 63, 88, 88, spt.Vec(), spt.Vec(1, 1, 1), spt.DIFF)) == bytes(ref[15])
+
+
+@pytest.mark.parametrize("w,h", [(512, 512), (256, 192), (1024, 768), (4096, 4096), (37, 11)])
+def test_camera_init_matches_reference_ctor(spt, oracle, w, h):
+    mine = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    ref = oracle.camera(float(np.float32(w) / np.float32(h)))
+    assert bytes(mine._c) == bytes(ref)
+
+
+def test_default_params_match_oracle(spt, oracle):
+    assert bytes(spt.default_params()) == bytes(oracle.default_params())
+
+
+@pytest.mark.parametrize("h,T,n", [(768, 8, 8), (768, 8, 1), (100, 8, 3), (7, 8, 2), (4096, 16, 8), (1, 8, 4)])
+def test_shard_rows_partition_the_image(spt, h, T, n):
+    seen = []
+    for k in range(n):
+        rows = spt.shard_rows(spt.default_params(height=h, tile_rows=T, shard_index=k, shard_count=n))
+        assert np.all(np.diff(rows) > 0)
+        assert all(((r // T) % n) == k for r in rows)
+        seen.extend(rows.tolist())
+    assert sorted(seen) == list(range(h))
+
+
+def test_invalid_arguments_fail_loudly(spt):
+    cam = spt.Camera(aspect=1.0)
+    with pytest.raises(spt.SptError) as e:
+        spt.render(spt.cornell_scene(), cam, spt.default_params(width=0))
+    assert e.value.status == 1
+    bad = spt.cornell_scene()
+    bad[3].refl = spt.SPEC
+    with pytest.raises(spt.SptError) as e:
+        spt.render(bad, cam, spt.default_params(width=8, height=8, spp=1))
+    assert e.value.status == 5
+
+
+def test_no_device_is_an_error_not_a_fallback(spt):
+    """Without a GPU (this container) rendering must fail with NO_DEVICE, never compute on CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(spt.SptError) as e:
+        spt.render(spt.cornell_scene(), spt.Camera(aspect=1.0), spt.default_params(width=8, height=8, spp=1))
+    assert e.value.status in (2, 3)
+
+
+def test_ppm_writer_byte_identical_to_reference_format(spt, oracle, tmp_path):
+    img = oracle.compat_render(64, 48, 4, seed=1, nee=True)
+    ref = open(os.path.join(ROOT, "tests", "golden", "ref_64x48_s4_nee.ppm"), "rb").read()
+    assert spt.ppm_bytes(img) == ref
