@@ -22,7 +22,6 @@ from __future__ import annotations
 import argparse
 import importlib
 import json
-import math
 import os
 import sys
 import time
@@ -57,9 +56,10 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
 
     threads = min(16, os.cpu_count() or 1)
     h, w, spp = params.height, params.width, params.spp
+    calib = np.linspace(0, h - 1, threads).astype(np.int32)  # one row per thread
     t0 = time.perf_counter()
-    oracle.counter_render(prims, cam._c, params, rows=np.array([h // 2], np.int32), threads=threads)
-    t_row = max(time.perf_counter() - t0, 1e-3)
+    oracle.counter_render(prims, cam._c, params, rows=calib, threads=threads)
+    t_row = max(time.perf_counter() - t0, 1e-3) / len(calib)
     n_rows = int(max(1, min(h, round(budget_s / t_row))))
     stride = max(1, h // n_rows)
     rows = np.arange(stride // 2, h, stride, dtype=np.int32)[:n_rows]
