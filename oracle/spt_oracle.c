@@ -413,42 +413,48 @@ typedef struct {
   uint32_t key[2];
 } c_ctx;
 
-/* The counter-mode scene intersection. inv = 1/d computed once per ray; ties keep the lowest index;
- * id is left untouched on a miss; returns 1 on hit with *t set, *t = 1e20f on a miss. */
+/* The counter-mode scene intersection (intersect :323-335). inv = 1/d is computed once per ray.
+ * Primitives are tested grouped by kind — all RECT_XY in index order, then RECT_XZ, RECT_YZ,
+ * SPHERE — with the reference's strict `<` (:328), so the first primitive in THAT order wins a
+ * tie of exactly equal t (the reference: lowest index; they differ only for bit-identical t from
+ * two different kinds). id is left untouched on a miss; returns 1 on hit, *t = 1e20f on a miss. */
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
   float tmin = 1e20f;
-  int i;
-  for (i = 0; i < C->n; i++) {
-    const c_prim* P = &C->prims[i];
-    float tt, a, b;
-    switch (P->kind) {
-      case SPT_RECT_XY:
-        tt = (P->k - o.z) * iz; a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y); break;
-      case SPT_RECT_XZ:
-        tt = (P->k - o.y) * iy; a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z); break;
-      case SPT_RECT_YZ:
-        tt = (P->k - o.x) * ix; a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z); break;
-      default: { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
-        const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
-        const float bb = fdot(op, d);
-        const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-        const float det = P->rad2 - fdot(q, q);
-        float sd, t1, t2;
-        if (!(det >= 0.0f)) continue;
-        sd = sqrtf(det);
-        t1 = bb - sd;
-        t2 = bb + sd;
-        tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
-        if (tt != 0.0f && tt < tmin) { tmin = tt; *id = i; }
-        continue;
+  int kind, i;
+  for (kind = SPT_RECT_XY; kind <= SPT_SPHERE; kind++) {
+    for (i = 0; i < C->n; i++) {
+      const c_prim* P = &C->prims[i];
+      float tt, a, b;
+      if (P->kind != kind) continue;
+      switch (kind) {
+        case SPT_RECT_XY:
+          tt = (P->k - o.z) * iz; a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y); break;
+        case SPT_RECT_XZ:
+          tt = (P->k - o.y) * iy; a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z); break;
+        case SPT_RECT_YZ:
+          tt = (P->k - o.x) * ix; a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z); break;
+        default: { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
+          const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
+          const float bb = fdot(op, d);
+          const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+          const float det = P->rad2 - fdot(q, q);
+          float sd, t1, t2;
+          if (!(det >= 0.0f)) continue;
+          sd = sqrtf(det);
+          t1 = bb - sd;
+          t2 = bb + sd;
+          tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+          if (tt != 0.0f && tt < tmin) { tmin = tt; *id = i; }
+          continue;
+        }
       }
-    }
-    /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin; for finite
-     * a, b (always, once tt < tmin) that is exactly the conjunction below. */
-    if (a >= P->b1 && a <= P->b2 && b >= P->c1 && b <= P->c2 && tt > 0.0f && tt < tmin) {
-      tmin = tt;
-      *id = i;
+      /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin; for finite
+       * a, b (always, once tt < tmin) that is exactly the conjunction below. */
+      if (a >= P->b1 && a <= P->b2 && b >= P->c1 && b <= P->c2 && tt > 0.0f && tt < tmin) {
+        tmin = tt;
+        *id = i;
+      }
     }
   }
   *t = tmin;

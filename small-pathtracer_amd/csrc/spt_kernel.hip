@@ -43,8 +43,22 @@ struct alignas(16) DevPrim {
 };
 static_assert(sizeof(DevPrim) == 64, "DevPrim layout");
 
+// Intersection geometry, grouped by kind (XY, XZ, YZ rects, then spheres; index order inside a
+// group) and read through the constant address space so every load in the intersect loop is a
+// wave-uniform s_load (scalar cache broadcast) — never a per-lane memory access.
+struct GeoRect { float k, b1, b2, c1, c2; int idx; int pad0, pad1; };   // 32 B
+struct GeoSph { float px, py, pz, rad2; int idx; int pad0, pad1, pad2; };  // 32 B
+struct SceneGeo {
+  int n_xy, n_xz, n_yz, n_sph;
+  int pad[4];
+  GeoRect rect[kMaxPrims];  // [0,n_xy) XY, [n_xy, n_xy+n_xz) XZ, then YZ
+  GeoSph sph[kMaxPrims];
+};
+#define SPT_CONST __attribute__((address_space(4)))
+
 struct KParams {
   const DevPrim* prims;
+  const SceneGeo* geo;
   int n_prims;
   float cam[12];  // origin, lower_left_corner, horizontal, vertical
   int width, height, spp;
@@ -64,39 +78,47 @@ struct KParams {
 };
 
 // Scene intersection of the counter-mode contract (intersect :323-335 over Rectangle_* :102-112 /
-// Sphere :229-239). Uniform loop over primitives: every read of P.prims[i] is wave-uniform and
-// becomes a scalar (s_load) broadcast. Ties keep the lowest index; id untouched on a miss.
+// Sphere :229-239): grouped kind order, strict `<`, id untouched on a miss (oracle c_intersect).
+template <int AXIS>
+__device__ __forceinline__ void rect_group(const SPT_CONST GeoRect* g, int n, float oa, float ia,
+                                           float db, float ob, float dc, float oc, float& tmin,
+                                           int& id) {
+#pragma unroll 2
+  for (int j = 0; j < n; ++j) {
+    int idx = g[j].idx;
+    asm volatile("" : "+s"(idx));  // keep the (uniform) index load unconditional, in an SGPR
+    const float tt = (g[j].k - oa) * ia;
+    const float a = fmaf(db, tt, ob), b = fmaf(dc, tt, oc);
+    const bool acc = (a >= g[j].b1) & (a <= g[j].b2) & (b >= g[j].c1) & (b <= g[j].c2) &
+                     (tt > 0.0f) & (tt < tmin);
+    tmin = acc ? tt : tmin;
+    id = acc ? idx : id;
+  }
+}
+
 __device__ __forceinline__ bool intersect_scene(const KParams& P, f3 o, f3 d, float& t_out,
                                                 int& id) {
   const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
   float tmin = 1e20f;
-  const DevPrim* __restrict__ S = P.prims;
-  for (int i = 0; i < P.n_prims; ++i) {
-    const int kind = S[i].kind;
-    float tt, a, b;
-    if (kind == SPT_RECT_XY) {
-      tt = (S[i].w1 - o.z) * iz; a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y);
-    } else if (kind == SPT_RECT_XZ) {
-      tt = (S[i].w1 - o.y) * iy; a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z);
-    } else if (kind == SPT_RECT_YZ) {
-      tt = (S[i].w1 - o.x) * ix; a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z);
-    } else {  // sphere, det = r^2 - |op - b d|^2
-      const f3 op = mk(S[i].w1 - o.x, S[i].w2 - o.y, S[i].w3 - o.z);
-      const float bb = dot3(op, d);
-      const f3 q = mk(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-      const float det = S[i].w4 - dot3(q, q);
-      if (det >= 0.0f) {
-        const float sd = sqrtf(det);
-        const float t1 = bb - sd, t2 = bb + sd;
-        const float ts = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
-        if (ts != 0.0f && ts < tmin) { tmin = ts; id = i; }
-      }
-      continue;
+  const SPT_CONST SceneGeo* G = (const SPT_CONST SceneGeo*)P.geo;
+  const int nxy = G->n_xy, nxz = G->n_xz, nyz = G->n_yz, nsph = G->n_sph;
+  rect_group<2>(G->rect, nxy, o.z, iz, d.x, o.x, d.y, o.y, tmin, id);
+  rect_group<1>(G->rect + nxy, nxz, o.y, iy, d.x, o.x, d.z, o.z, tmin, id);
+  rect_group<0>(G->rect + nxy + nxz, nyz, o.x, ix, d.y, o.y, d.z, o.z, tmin, id);
+  for (int j = 0; j < nsph; ++j) {  // det = r^2 - |op - b d|^2
+    const SPT_CONST GeoSph& S = G->sph[j];
+    const f3 op = mk(S.px - o.x, S.py - o.y, S.pz - o.z);
+    const float bb = dot3(op, d);
+    const f3 q = mk(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+    const float det = S.rad2 - dot3(q, q);
+    if (det >= 0.0f) {
+      const float sd = sqrtf(det);
+      const float t1 = bb - sd, t2 = bb + sd;
+      const float ts = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+      const bool acc = (ts != 0.0f) & (ts < tmin);
+      tmin = acc ? ts : tmin;
+      id = acc ? S.idx : id;
     }
-    const bool acc = (a >= S[i].w2) & (a <= S[i].w3) & (b >= S[i].w4) & (b <= S[i].w5) &
-                     (tt > 0.0f) & (tt < tmin);
-    tmin = acc ? tt : tmin;
-    id = acc ? i : id;
   }
   t_out = tmin;
   return tmin < 1e20f;
@@ -375,6 +397,7 @@ struct spt_context {
   int device = 0;
   int n_cu = 0, blocks_per_cu = 0;
   DevPrim* prims = nullptr;
+  SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
   size_t accum_cap = 0;  // elements
   uint32_t* queue = nullptr;
@@ -383,6 +406,9 @@ struct spt_context {
   bool pending = false;
   int n_prims = 0;
   KParams last{};
+  // Pinned staging for the async scene upload; reused only after the previous upload completed.
+  DevPrim* h_prims = nullptr;
+  SceneGeo* h_geo = nullptr;
 };
 
 extern "C" int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
@@ -435,6 +461,32 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
   }
 }
 
+static void build_geo(const spt_prim* s, int n, SceneGeo* g) {
+  std::memset(g, 0, sizeof *g);
+  int r = 0;
+  const int kinds[3] = {SPT_RECT_XY, SPT_RECT_XZ, SPT_RECT_YZ};
+  int* counts[3] = {&g->n_xy, &g->n_xz, &g->n_yz};
+  for (int k = 0; k < 3; ++k) {
+    for (int i = 0; i < n; ++i) {
+      if (s[i].kind != kinds[k]) continue;
+      GeoRect& R = g->rect[r++];
+      R.k = (float)s[i].geom[4];
+      R.b1 = (float)s[i].geom[0]; R.b2 = (float)s[i].geom[1];
+      R.c1 = (float)s[i].geom[2]; R.c2 = (float)s[i].geom[3];
+      R.idx = i;
+      ++*counts[k];
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    if (s[i].kind != SPT_SPHERE) continue;
+    GeoSph& S = g->sph[g->n_sph++];
+    const float rad = (float)s[i].geom[0];
+    S.px = (float)s[i].geom[1]; S.py = (float)s[i].geom[2]; S.pz = (float)s[i].geom[3];
+    S.rad2 = rad * rad;
+    S.idx = i;
+  }
+}
+
 static int tile_rows_of(const spt_params* p) { return p->tile_rows > 0 ? p->tile_rows : 8; }
 
 extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
@@ -457,6 +509,9 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
     bpc = 4;
   c->blocks_per_cu = bpc;
   hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
+  if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_geo, sizeof(SceneGeo), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(&c->queue, sizeof(uint32_t) * 64);
   if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * 8);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -473,6 +528,9 @@ extern "C" spt_status spt_context_destroy(spt_context* c) {
   if (!c) return SPT_OK;
   (void)hipSetDevice(c->device);
   if (c->prims) (void)hipFree(c->prims);
+  if (c->geo) (void)hipFree(c->geo);
+  if (c->h_prims) (void)hipHostFree(c->h_prims);
+  if (c->h_geo) (void)hipHostFree(c->h_geo);
   if (c->accum) (void)hipFree(c->accum);
   if (c->queue) (void)hipFree(c->queue);
   if (c->stats) (void)hipFree(c->stats);
@@ -509,11 +567,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   hipStream_t stream = (hipStream_t)stream_v;
 
   KParams K{};
-  DevPrim host_prims[kMaxPrims];
-  to_dev(prims, n_prims, host_prims);
-  SPT_HIP(hipMemcpyAsync(c->prims, host_prims, sizeof(DevPrim) * n_prims, hipMemcpyHostToDevice,
+  if (c->pending) SPT_HIP(hipEventSynchronize(c->ev0));  // staging still read by a prior upload
+  to_dev(prims, n_prims, c->h_prims);
+  build_geo(prims, n_prims, c->h_geo);
+  SPT_HIP(hipMemcpyAsync(c->prims, c->h_prims, sizeof(DevPrim) * n_prims, hipMemcpyHostToDevice,
                          stream));
+  SPT_HIP(hipMemcpyAsync(c->geo, c->h_geo, sizeof(SceneGeo), hipMemcpyHostToDevice, stream));
   K.prims = c->prims;
+  K.geo = c->geo;
   K.n_prims = n_prims;
   for (int i = 0; i < 3; ++i) {
     K.cam[i] = (float)cam->origin[i];
