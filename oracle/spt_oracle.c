@@ -357,8 +357,35 @@ typedef struct { float x, y, z; } fv;
 static inline fv fv3(float x, float y, float z) { fv r = {x, y, z}; return r; }
 static inline float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
 static inline float fdot(fv a, fv b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+/* Deterministic reciprocal / rsqrt of the contract: integer seed + 3 Newton steps (only IEEE
+ * fma/mul and integer ops, so every platform computes the same bits). */
+static inline float asf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t asu(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+float spt_oracle_rcp_nr(float x) {
+  float y = asf(0x7EF311C3u - asu(x));
+  int i;
+  for (i = 0; i < 3; i++) {
+    const float e = fmaf(-x, y, 1.0f);
+    y = fmaf(e, y, y);
+  }
+  return y;
+}
+float spt_oracle_rsq_nr(float x) {
+  float y = asf(0x5F375A86u - (asu(x) >> 1));
+  const float h = 0.5f * x;
+  int i;
+  for (i = 0; i < 3; i++) {
+    const float hy = h * y;
+    y = y * fmaf(-hy, y, 1.5f);
+  }
+  return y;
+}
+/* Vec::norm :50-52 as v * rsq(len2); exactly-unit vectors are returned unchanged. */
 static inline fv fnormalize(fv v) {
-  const float inv = 1.0f / sqrtf(fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x)));
+  const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+  float inv;
+  if (l2 == 1.0f) return v;
+  inv = spt_oracle_rsq_nr(l2);
   return fv3(v.x * inv, v.y * inv, v.z * inv);
 }
 static inline fv fcross(fv a, fv b) {
@@ -413,13 +440,13 @@ typedef struct {
   uint32_t key[2];
 } c_ctx;
 
-/* The counter-mode scene intersection (intersect :323-335). inv = 1/d is computed once per ray.
+/* The counter-mode scene intersection (intersect :323-335). inv = rcp_nr(d) once per ray.
  * Primitives are tested grouped by kind — all RECT_XY in index order, then RECT_XZ, RECT_YZ,
  * SPHERE — with the reference's strict `<` (:328), so the first primitive in THAT order wins a
  * tie of exactly equal t (the reference: lowest index; they differ only for bit-identical t from
  * two different kinds). id is left untouched on a miss; returns 1 on hit, *t = 1e20f on a miss. */
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
-  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  const float ix = spt_oracle_rcp_nr(d.x), iy = spt_oracle_rcp_nr(d.y), iz = spt_oracle_rcp_nr(d.z);
   float tmin = 1e20f;
   int kind, i;
   for (kind = SPT_RECT_XY; kind <= SPT_SPHERE; kind++) {
@@ -467,8 +494,8 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb) {
   fv a, u, v;
   float r2s, s1, cr, sr;
   spt_oracle_sincos2pi(xi1, &s, &c);
-  r2s = sqrtf(xi2);
-  s1 = sqrtf(1.0f - xi2);
+  r2s = xi2 * spt_oracle_rsq_nr(xi2);
+  s1 = (1.0f - xi2) * spt_oracle_rsq_nr(1.0f - xi2);
   a = fabsf(nl.x) > 0.1f ? fv3(nl.z, 0.0f, -nl.x) : fv3(0.0f, -nl.z, nl.y);
   u = fnormalize(a);
   v = fcross(nl, u);

@@ -1,9 +1,15 @@
 // spt_device.h — device-side building blocks of the counter-mode contract (gfx950).
 //
 // Every float operation here is spelled exactly as in the contract (DESIGN.md "Counter-mode
-// contract"): explicit fmaf, IEEE correctly rounded '/' and sqrtf (built with
-// -fhip-fp32-correctly-rounded-divide-sqrt -ffp-contract=off), no fast-math, so the kernel
-// reproduces the CPU statement of the same contract bit for bit.
+// contract", restated on the CPU in oracle/spt_oracle.c): explicit fmaf, IEEE '/' where the
+// contract keeps a true division, integer-seeded Newton-Raphson reciprocal / rsqrt elsewhere,
+// no fast-math and no implicit contraction (-ffp-contract=off), so the kernel reproduces the CPU
+// statement of the same contract bit for bit.
+//
+// Cost model on gfx950 (tools/valu_rates.hip, measured): add/mul/fma/xor/cmp full rate (2 cyc per
+// wave64 instruction per SIMD); v_mad_u64_u32, v_mul_lo/hi_u32, packed fp32 half rate; v_rcp /
+// v_sqrt / v_sin quarter rate. A correctly rounded fp32 '/' or sqrtf is a ~30-cycle sequence;
+// rcp_nr / rsq_nr below are 7 / 11 full-rate instructions.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,12 +25,16 @@ struct u4 { uint32_t x, y, z, w; };
 
 __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1) {
+  // Keep the key opaque so the (wave-uniform) key schedule is recomputed with SALU adds per call
+  // instead of being hoisted into 20 live SGPRs.
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(kPhM0, c0), lo0 = kPhM0 * c0;
-    const uint32_t hi1 = __umulhi(kPhM1, c2), lo1 = kPhM1 * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    const uint64_t p0 = (uint64_t)kPhM0 * c0;  // one v_mad_u64_u32 each (hi and lo together)
+    const uint64_t p1 = (uint64_t)kPhM1 * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     k0 += kPhW0; k1 += kPhW1;
   }
   return u4{c0, c1, c2, c3};
@@ -32,12 +42,37 @@ __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
 
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
 
+// ---- deterministic reciprocal / reciprocal square root (contract): integer seed + 3 Newton
+// steps; max relative error 6e-8 / 1.3e-7 (oracle tests). rcp_nr(+-0) is NaN, which the
+// intersection treats exactly like 1/0 = inf (no hit on a parallel plane).
+__device__ __forceinline__ float rcp_nr(float x) {
+  float y = __uint_as_float(0x7EF311C3u - __float_as_uint(x));
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float e = fmaf(-x, y, 1.0f);
+    y = fmaf(e, y, y);
+  }
+  return y;
+}
+__device__ __forceinline__ float rsq_nr(float x) {
+  float y = __uint_as_float(0x5F375A86u - (__float_as_uint(x) >> 1));
+  const float h = 0.5f * x;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float hy = h * y;
+    y = y * fmaf(-hy, y, 1.5f);
+  }
+  return y;
+}
+
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-// Vec::norm :50-52 as *this * (1/sqrt(len2)).
+// Vec::norm :50-52 as *this * rsq(len2); exactly-unit vectors are returned unchanged.
 __device__ __forceinline__ f3 normalize3(f3 v) {
-  const float inv = 1.0f / sqrtf(fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x)));
+  const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+  if (l2 == 1.0f) return v;
+  const float inv = rsq_nr(l2);
   return mk(v.x * inv, v.y * inv, v.z * inv);
 }
 // operator% :56-58
@@ -72,8 +107,9 @@ __device__ __forceinline__ f3 cosine_dir(f3 nl, uint32_t ra, uint32_t rb) {
   const float xi1 = u01(ra), xi2 = u01(rb);
   float s, c;
   sincos2pi(xi1, s, c);
-  const float r2s = sqrtf(xi2);
-  const float s1 = sqrtf(1.0f - xi2);
+  const float r2s = xi2 * rsq_nr(xi2);  // sqrt(r2); xi2 = 0 gives 0
+  const float om = 1.0f - xi2;
+  const float s1 = om * rsq_nr(om);     // sqrt(1 - r2)
   const f3 a = fabsf(nl.x) > 0.1f ? mk(nl.z, 0.0f, -nl.x) : mk(0.0f, -nl.z, nl.y);
   const f3 u = normalize3(a);
   const f3 v = cross3(nl, u);

@@ -56,7 +56,7 @@ struct SceneGeo {
 };
 #define SPT_CONST __attribute__((address_space(4)))
 
-struct KParams {
+struct KParams {  // in device memory, read through a laundered constant-space pointer
   const DevPrim* prims;
   const SceneGeo* geo;
   int n_prims;
@@ -72,18 +72,28 @@ struct KParams {
   int chunk, n_local_pix;
   uint32_t n_units;
   float inv_spp;
+  // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
+  // always ends there (RR with p == 0, :448), so the NEE test only needs "is the nearest hit the
+  // light" — an occlusion query without id bookkeeping.
+  int light_black, light_kind, light_pos;
   unsigned long long* accum;  // [n_local_pix][3] 32.32 fixed point
   uint32_t* queue;            // [0] = next unit
   unsigned long long* stats;  // [8]
 };
 
+// Re-derive a wave-uniform pointer as opaque so uniform loads are re-issued (s_load) where used
+// instead of being hoisted into long-lived SGPRs (which spill to VGPR lanes).
+template <typename T>
+__device__ __forceinline__ const SPT_CONST T* cptr(const T* p) {
+  asm volatile("" : "+s"(p));
+  return (const SPT_CONST T*)p;
+}
+
 // Scene intersection of the counter-mode contract (intersect :323-335 over Rectangle_* :102-112 /
 // Sphere :229-239): grouped kind order, strict `<`, id untouched on a miss (oracle c_intersect).
-template <int AXIS>
 __device__ __forceinline__ void rect_group(const SPT_CONST GeoRect* g, int n, float oa, float ia,
                                            float db, float ob, float dc, float oc, float& tmin,
                                            int& id) {
-#pragma unroll 2
   for (int j = 0; j < n; ++j) {
     int idx = g[j].idx;
     asm volatile("" : "+s"(idx));  // keep the (uniform) index load unconditional, in an SGPR
@@ -96,32 +106,94 @@ __device__ __forceinline__ void rect_group(const SPT_CONST GeoRect* g, int n, fl
   }
 }
 
-__device__ __forceinline__ bool intersect_scene(const KParams& P, f3 o, f3 d, float& t_out,
-                                                int& id) {
-  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+__device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d) {
+  // det = r^2 - |op - b d|^2; nearest root beyond the fp32 epsilon (Sphere::intersect :229-239)
+  const f3 op = mk(S.px - o.x, S.py - o.y, S.pz - o.z);
+  const float bb = dot3(op, d);
+  const f3 q = mk(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+  const float det = S.rad2 - dot3(q, q);
+  if (!(det >= 0.0f)) return 0.0f;
+  const float sd = sqrtf(det);
+  const float t1 = bb - sd, t2 = bb + sd;
+  return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+}
+
+__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, f3 o, f3 d,
+                                                float& t_out, int& id) {
+  const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
   float tmin = 1e20f;
-  const SPT_CONST SceneGeo* G = (const SPT_CONST SceneGeo*)P.geo;
   const int nxy = G->n_xy, nxz = G->n_xz, nyz = G->n_yz, nsph = G->n_sph;
-  rect_group<2>(G->rect, nxy, o.z, iz, d.x, o.x, d.y, o.y, tmin, id);
-  rect_group<1>(G->rect + nxy, nxz, o.y, iy, d.x, o.x, d.z, o.z, tmin, id);
-  rect_group<0>(G->rect + nxy + nxz, nyz, o.x, ix, d.y, o.y, d.z, o.z, tmin, id);
-  for (int j = 0; j < nsph; ++j) {  // det = r^2 - |op - b d|^2
-    const SPT_CONST GeoSph& S = G->sph[j];
-    const f3 op = mk(S.px - o.x, S.py - o.y, S.pz - o.z);
-    const float bb = dot3(op, d);
-    const f3 q = mk(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-    const float det = S.rad2 - dot3(q, q);
-    if (det >= 0.0f) {
-      const float sd = sqrtf(det);
-      const float t1 = bb - sd, t2 = bb + sd;
-      const float ts = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
-      const bool acc = (ts != 0.0f) & (ts < tmin);
-      tmin = acc ? ts : tmin;
-      id = acc ? S.idx : id;
-    }
+  rect_group(G->rect, nxy, o.z, iz, d.x, o.x, d.y, o.y, tmin, id);
+  rect_group(G->rect + nxy, nxz, o.y, iy, d.x, o.x, d.z, o.z, tmin, id);
+  rect_group(G->rect + nxy + nxz, nyz, o.x, ix, d.y, o.y, d.z, o.z, tmin, id);
+  for (int j = 0; j < nsph; ++j) {
+    int idx = G->sph[j].idx;
+    asm volatile("" : "+s"(idx));
+    const float ts = sphere_t(G->sph[j], o, d);
+    const bool acc = (ts != 0.0f) & (ts < tmin);
+    tmin = acc ? ts : tmin;
+    id = acc ? idx : id;
   }
   t_out = tmin;
   return tmin < 1e20f;
+}
+
+// Occluders of one rect segment [b, e) of the grouped array: accepted with t < thr.
+__device__ __forceinline__ bool occl_rects(const SPT_CONST GeoRect* g, int b, int e, float oa,
+                                           float ia, float db, float ob, float dc, float oc,
+                                           float thr, bool occ) {
+  for (int j = b; j < e; ++j) {
+    const float tt = (g[j].k - oa) * ia;
+    const float a = fmaf(db, tt, ob), c = fmaf(dc, tt, oc);
+    occ |= (a >= g[j].b1) & (a <= g[j].b2) & (c >= g[j].c1) & (c <= g[j].c2) & (tt > 0.0f) &
+           (tt < thr);
+  }
+  return occ;
+}
+
+// NEE shadow test for a black light: identical outcome to intersect_scene() followed by
+// `id == light` (:466-467) — the light at grouped position L wins iff it is accepted at t_L, no
+// primitive before it in grouped order is accepted with t <= t_L and none after it with t < t_L.
+__device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
+                                                  const SPT_CONST SceneGeo* G, f3 o, f3 d,
+                                                  float& tL) {
+  const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
+  const int nxy = G->n_xy, nxz = G->n_xz, nyz = G->n_yz, nsph = G->n_sph;
+  const int lk = P->light_kind, lp = P->light_pos;
+  bool ok;
+  if (lk == SPT_SPHERE) {
+    tL = sphere_t(G->sph[lp], o, d);
+    ok = (tL != 0.0f) & (tL < 1e20f);
+  } else {
+    const SPT_CONST GeoRect& R = G->rect[lp];
+    float oa, ia, db, ob, dc, oc;
+    if (lk == SPT_RECT_XY) { oa = o.z; ia = iz; db = d.x; ob = o.x; dc = d.y; oc = o.y; }
+    else if (lk == SPT_RECT_XZ) { oa = o.y; ia = iy; db = d.x; ob = o.x; dc = d.z; oc = o.z; }
+    else { oa = o.x; ia = ix; db = d.y; ob = o.y; dc = d.z; oc = o.z; }
+    tL = (R.k - oa) * ia;
+    const float a = fmaf(db, tL, ob), c = fmaf(dc, tL, oc);
+    ok = (a >= R.b1) & (a <= R.b2) & (c >= R.c1) & (c <= R.c2) & (tL > 0.0f) & (tL < 1e20f);
+  }
+  if (__ballot(ok) == 0) return false;
+  const float before = __uint_as_float(__float_as_uint(tL) + 1u);  // t <= tL  <=>  t < next-up(tL)
+  const int nrect = nxy + nxz + nyz;
+  const int L = lk == SPT_SPHERE ? nrect : lp;  // rect positions < L are "before" the light
+  bool occ = false;
+  const int e1 = nxy, e2 = nxy + nxz;
+  // XY [0,e1), XZ [e1,e2), YZ [e2,nrect): split each at the light position
+  occ = occl_rects(G->rect, 0, min(e1, L), o.z, iz, d.x, o.x, d.y, o.y, before, occ);
+  occ = occl_rects(G->rect, max(0, L + 1), e1, o.z, iz, d.x, o.x, d.y, o.y, tL, occ);
+  occ = occl_rects(G->rect, e1, min(e2, L), o.y, iy, d.x, o.x, d.z, o.z, before, occ);
+  occ = occl_rects(G->rect, max(e1, L + 1), e2, o.y, iy, d.x, o.x, d.z, o.z, tL, occ);
+  occ = occl_rects(G->rect, e2, min(nrect, L), o.x, ix, d.y, o.y, d.z, o.z, before, occ);
+  occ = occl_rects(G->rect, max(e2, L + 1), nrect, o.x, ix, d.y, o.y, d.z, o.z, tL, occ);
+  const int ls = lk == SPT_SPHERE ? lp : -1;  // sphere positions < ls are before the light
+  for (int j = 0; j < nsph; ++j) {
+    if (j == ls) continue;
+    const float ts = sphere_t(G->sph[j], o, d);
+    occ |= (ts != 0.0f) & (ts < (j < ls ? before : tL));
+  }
+  return ok & !occ;
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -129,9 +201,12 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-__global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
+__global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
-  for (int i = threadIdx.x; i < P.n_prims; i += kBlock) s_prims[i] = P.prims[i];
+  {
+    const SPT_CONST KParams* P = cptr(Pg);
+    for (int i = threadIdx.x; i < P->n_prims; i += kBlock) s_prims[i] = P->prims[i];
+  }
   __syncthreads();
 
   const uint32_t lane = __lane_id();
@@ -145,13 +220,13 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
   // ---- wave-uniform state
   uint32_t pool_next = 0, pool_end = 0;
   bool exhausted = false;
-  uint32_t n_samples = 0, n_path = 0, n_shadow = 0, n_vert = 0, n_nee = 0, n_nee_hit = 0,
-           n_cos = 0, n_miss = 0;
+  uint32_t n_path = 0, n_shadow = 0, n_vert = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
 
   for (;;) {
+    const SPT_CONST KParams* P = cptr(Pg);
     // 1) retire finished units: flush the fixed-point sums of their pixel.
     if (has_unit && need_cam && s >= s_end) {
-      unsigned long long* a = P.accum + 3ull * lp;
+      unsigned long long* a = P->accum + 3ull * lp;
       if (acc0) atomicAdd(a + 0, acc0);
       if (acc1) atomicAdd(a + 1, acc1);
       if (acc2) atomicAdd(a + 2, acc2);
@@ -162,28 +237,30 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
     bool needs_unit = !has_unit;
     uint64_t need = __ballot(needs_unit);
     while (need != 0 && !exhausted) {
+      const SPT_CONST KParams* Q = cptr(Pg);
       if (pool_next >= pool_end) {
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(P.queue, kGrab);
+        if (lane == 0) b = atomicAdd(Q->queue, kGrab);
         b = __builtin_amdgcn_readfirstlane(b);
-        if (b >= P.n_units) { exhausted = true; break; }
+        if (b >= Q->n_units) { exhausted = true; break; }
         pool_next = b;
-        pool_end = min(b + kGrab, P.n_units);
+        pool_end = min(b + kGrab, Q->n_units);
       }
       const uint32_t rank = lane_rank(need);
       const uint32_t avail = pool_end - pool_next;
       if (needs_unit && rank < avail) {
         const uint32_t u = pool_next + rank;
-        const uint32_t j = u / (uint32_t)P.n_local_pix;  // chunk-major: lanes get adjacent pixels
-        lp = u - j * (uint32_t)P.n_local_pix;
-        s = j * (uint32_t)P.chunk;
-        s_end = min(s + (uint32_t)P.chunk, (uint32_t)P.spp);
-        const uint32_t lr = lp / (uint32_t)P.width;
-        px = (int)(lp - lr * (uint32_t)P.width);
-        const uint32_t tile = lr / (uint32_t)P.tile_rows, within = lr - tile * (uint32_t)P.tile_rows;
-        py = (int)((tile * (uint32_t)P.shard_count + (uint32_t)P.shard_index) *
-                       (uint32_t)P.tile_rows + within);
-        pix = (uint32_t)py * (uint32_t)P.width + (uint32_t)px;
+        const uint32_t npix = (uint32_t)Q->n_local_pix, w = (uint32_t)Q->width;
+        const uint32_t j = u / npix;  // chunk-major: lanes get adjacent pixels
+        lp = u - j * npix;
+        s = j * (uint32_t)Q->chunk;
+        s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
+        const uint32_t lr = lp / w;
+        px = (int)(lp - lr * w);
+        const uint32_t T_ = (uint32_t)Q->tile_rows;
+        const uint32_t tile = lr / T_, within = lr - tile * T_;
+        py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
+        pix = (uint32_t)py * w + (uint32_t)px;
         has_unit = true;
         needs_unit = false;
         need_cam = true;
@@ -194,25 +271,25 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
     if (__ballot(has_unit) == 0) break;
 
     // per-lane events of this iteration, counted by ballots at the convergent end of the loop
-    bool ev_cam = false, ev_path = false, ev_miss = false, ev_vert2 = false, ev_nee = false,
-         ev_nee_hit = false, ev_cos = false;
+    bool ev_path = false, ev_miss = false, ev_vert2 = false, ev_nee = false, ev_nee_hit = false,
+         ev_cos = false;
     const bool ev_vert = has_unit;
     if (has_unit) {
       // 3) camera ray for lanes starting a sample (:533-536).
       if (need_cam) {
-        const u4 r = philox4x32_10(pix, s, 0u, 0u, P.key0, P.key1);
-        const float su = (((float)px - 0.5f) + u01(r.x)) / (float)P.width;
-        const float sv = (((float)(P.height - py - 1) - 0.5f) + u01(r.y)) / (float)P.height;
-        o = mk(P.cam[0], P.cam[1], P.cam[2]);
-        d = normalize3(mk(fmaf(P.cam[9], sv, fmaf(P.cam[6], su, P.cam[3])) - P.cam[0],
-                          fmaf(P.cam[10], sv, fmaf(P.cam[7], su, P.cam[4])) - P.cam[1],
-                          fmaf(P.cam[11], sv, fmaf(P.cam[8], su, P.cam[5])) - P.cam[2]));
+        const SPT_CONST KParams* C = cptr(Pg);
+        const u4 r = philox4x32_10(pix, s, 0u, 0u, C->key0, C->key1);
+        const float su = (((float)px - 0.5f) + u01(r.x)) / (float)C->width;
+        const float sv = (((float)(C->height - py - 1) - 0.5f) + u01(r.y)) / (float)C->height;
+        o = mk(C->cam[0], C->cam[1], C->cam[2]);
+        d = normalize3(mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
+                          fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
+                          fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]));
         T = mk(1, 1, 1);
         L = mk(0, 0, 0);
         depth = 0;
         carried = false;
         need_cam = false;
-        ev_cam = true;
       }
       // 4) vertex: hittingPoint :371-377 (or the hit carried from a NEE shadow ray).
       int id = 0;
@@ -222,7 +299,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
         hit = c_hit; t = c_t; id = hit ? c_id : 0;
         carried = false;
       } else {
-        hit = intersect_scene(P, o, d, t, id);
+        hit = intersect_scene(cptr(P->geo), o, d, t, id);
         ev_path = true;
       }
       const DevPrim& H = s_prims[id];
@@ -252,15 +329,17 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
       ++depth;
       // Russian roulette :448-454 (+ optional hard depth cap).
       bool term = false;
-      if (P.max_depth > 0 && depth >= P.max_depth) {
+      const int max_depth = P->max_depth;
+      if (max_depth > 0 && depth >= max_depth) {
         term = true;
-      } else if (depth > P.rr_depth || p == 0.0f) {
+      } else if (depth > P->rr_depth || p == 0.0f) {
         if (!(p > 0.0f)) {
           term = true;
         } else {
           bool keep = true;
           if (p < 1.0f) {
-            const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, P.key0, P.key1);
+            const SPT_CONST KParams* C = cptr(Pg);
+            const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, C->key0, C->key1);
             keep = u01(r.x) < p;
           }
           if (keep) {
@@ -273,14 +352,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
       }
       if (!term) {
         // DIFF :457-480.
+        const SPT_CONST KParams* C = cptr(Pg);
         bool nee;
-        if (P.nee_prob >= 1.0f) nee = true;
-        else if (P.nee_prob <= 0.0f) nee = false;
+        const float q = C->nee_prob;
+        if (q >= 1.0f) nee = true;
+        else if (q <= 0.0f) nee = false;
         else {
-          const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, P.key0, P.key1);
-          nee = u01(r.y) < P.nee_prob;
+          const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, C->key0, C->key1);
+          nee = u01(r.y) < q;
         }
-        const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 0u, P.key0, P.key1);
+        const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 0u, C->key0, C->key1);
         float w = 1.0f;
         f3 dn;
         bool light_end = false;
@@ -288,22 +369,31 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
         bool scatter = true;
         if (nee) {
           // light_sampling :363-369, shadow ray :466, NEE weight :471-472.
+          const SPT_CONST KParams* D = cptr(Pg);
           float xl, zl;
-          if (P.light_mode == SPT_LIGHT_GLIBC_WRAP) {
-            xl = fmaf((float)(int32_t)((r.x >> 1) * P.ldxi), 0x1p-31f, P.lx0);
-            zl = fmaf((float)(int32_t)((r.y >> 1) * P.ldzi), 0x1p-31f, P.lz0);
+          if (D->light_mode == SPT_LIGHT_GLIBC_WRAP) {
+            xl = fmaf((float)(int32_t)((r.x >> 1) * D->ldxi), 0x1p-31f, D->lx0);
+            zl = fmaf((float)(int32_t)((r.y >> 1) * D->ldzi), 0x1p-31f, D->lz0);
           } else {
-            xl = fmaf(u01(r.x), P.ldx, P.lx0);
-            zl = fmaf(u01(r.y), P.ldz, P.lz0);
+            xl = fmaf(u01(r.x), D->ldx, D->lx0);
+            zl = fmaf(u01(r.y), D->ldz, D->lz0);
           }
-          const f3 dl = normalize3(mk(xl - x.x, P.ly - x.y, zl - x.z));
-          int ids = id;
+          const f3 dl = normalize3(mk(xl - x.x, D->ly - x.y, zl - x.z));
+          const int light_id = D->light_id;
           float ts;
-          const bool sh = intersect_scene(P, x, dl, ts, ids);
+          bool to_light, sh = true;
+          int ids = light_id;
+          if (D->light_black) {
+            to_light = shadow_hits_light(D, cptr(D->geo), x, dl, ts);
+          } else {
+            ids = id;
+            sh = intersect_scene(cptr(D->geo), x, dl, ts, ids);
+            to_light = ids == light_id;
+          }
           ev_nee = true;
-          if (ids == P.light_id) {
+          if (to_light) {
             ev_nee_hit = true;
-            const float pdf = fabsf((P.larea * dl.y) / (ts * ts));
+            const float pdf = fabsf((cptr(Pg)->larea * dl.y) / (ts * ts));
             const float brdf = fabsf(dot3(dl, nl) * 0.318309886183790672f);
             w = pdf * brdf;
             dn = dl;
@@ -335,31 +425,30 @@ __global__ void __launch_bounds__(kBlock) render_kernel(KParams P) {
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
       }
       if (term) {
-        acc0 += fix32(L.x, P.inv_spp);
-        acc1 += fix32(L.y, P.inv_spp);
-        acc2 += fix32(L.z, P.inv_spp);
+        const float inv_spp = cptr(Pg)->inv_spp;
+        acc0 += fix32(L.x, inv_spp);
+        acc1 += fix32(L.y, inv_spp);
+        acc2 += fix32(L.z, inv_spp);
         ++s;
         need_cam = true;
       }
     }
-    n_samples += (uint32_t)__popcll(__ballot(ev_cam));
     n_path += (uint32_t)__popcll(__ballot(ev_path));
     n_miss += (uint32_t)__popcll(__ballot(ev_miss));
     n_vert += (uint32_t)__popcll(__ballot(ev_vert)) + (uint32_t)__popcll(__ballot(ev_vert2));
-    n_nee += (uint32_t)__popcll(__ballot(ev_nee));
     n_shadow += (uint32_t)__popcll(__ballot(ev_nee));
     n_nee_hit += (uint32_t)__popcll(__ballot(ev_nee_hit));
     n_cos += (uint32_t)__popcll(__ballot(ev_cos));
   }
   if (lane == 0) {
-    atomicAdd(P.stats + 0, (unsigned long long)n_samples);
-    atomicAdd(P.stats + 1, (unsigned long long)n_path);
-    atomicAdd(P.stats + 2, (unsigned long long)n_shadow);
-    atomicAdd(P.stats + 3, (unsigned long long)n_vert);
-    atomicAdd(P.stats + 4, (unsigned long long)n_nee);
-    atomicAdd(P.stats + 5, (unsigned long long)n_nee_hit);
-    atomicAdd(P.stats + 6, (unsigned long long)n_cos);
-    atomicAdd(P.stats + 7, (unsigned long long)n_miss);
+    unsigned long long* st = cptr(Pg)->stats;
+    atomicAdd(st + 1, (unsigned long long)n_path);
+    atomicAdd(st + 2, (unsigned long long)n_shadow);
+    atomicAdd(st + 3, (unsigned long long)n_vert);
+    atomicAdd(st + 4, (unsigned long long)n_shadow);
+    atomicAdd(st + 5, (unsigned long long)n_nee_hit);
+    atomicAdd(st + 6, (unsigned long long)n_cos);
+    atomicAdd(st + 7, (unsigned long long)n_miss);
   }
 }
 
@@ -409,6 +498,10 @@ struct spt_context {
   // Pinned staging for the async scene upload; reused only after the previous upload completed.
   DevPrim* h_prims = nullptr;
   SceneGeo* h_geo = nullptr;
+  KParams* d_kp = nullptr;   // kernel parameters in device memory (read via s_load)
+  KParams* h_kp = nullptr;   // pinned staging
+  uint64_t samples = 0;      // pixel-samples of the last render (exact, not counted in-kernel)
+  double scene_flop = 0;     // FLOP-model cost of one ray against the scene
 };
 
 extern "C" int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
@@ -461,8 +554,10 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
   }
 }
 
-static void build_geo(const spt_prim* s, int n, SceneGeo* g) {
+// Grouped geometry; *light_pos = position of prim `light` in rect[] / sph[] (-1 if absent).
+static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* light_pos) {
   std::memset(g, 0, sizeof *g);
+  *light_pos = -1;
   int r = 0;
   const int kinds[3] = {SPT_RECT_XY, SPT_RECT_XZ, SPT_RECT_YZ};
   int* counts[3] = {&g->n_xy, &g->n_xz, &g->n_yz};
@@ -474,6 +569,7 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g) {
       R.b1 = (float)s[i].geom[0]; R.b2 = (float)s[i].geom[1];
       R.c1 = (float)s[i].geom[2]; R.c2 = (float)s[i].geom[3];
       R.idx = i;
+      if (i == light) *light_pos = r - 1;
       ++*counts[k];
     }
   }
@@ -484,6 +580,7 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g) {
     S.px = (float)s[i].geom[1]; S.py = (float)s[i].geom[2]; S.pz = (float)s[i].geom[3];
     S.rad2 = rad * rad;
     S.idx = i;
+    if (i == light) *light_pos = g->n_sph - 1;
   }
 }
 
@@ -512,6 +609,8 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc(&c->h_geo, sizeof(SceneGeo), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(&c->d_kp, sizeof(KParams));
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_kp, sizeof(KParams), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(&c->queue, sizeof(uint32_t) * 64);
   if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * 8);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -531,6 +630,8 @@ extern "C" spt_status spt_context_destroy(spt_context* c) {
   if (c->geo) (void)hipFree(c->geo);
   if (c->h_prims) (void)hipHostFree(c->h_prims);
   if (c->h_geo) (void)hipHostFree(c->h_geo);
+  if (c->d_kp) (void)hipFree(c->d_kp);
+  if (c->h_kp) (void)hipHostFree(c->h_kp);
   if (c->accum) (void)hipFree(c->accum);
   if (c->queue) (void)hipFree(c->queue);
   if (c->stats) (void)hipFree(c->stats);
@@ -569,7 +670,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   KParams K{};
   if (c->pending) SPT_HIP(hipEventSynchronize(c->ev0));  // staging still read by a prior upload
   to_dev(prims, n_prims, c->h_prims);
-  build_geo(prims, n_prims, c->h_geo);
+  int light_pos = -1;
+  build_geo(prims, n_prims, c->h_geo, p->light_id, &light_pos);
   SPT_HIP(hipMemcpyAsync(c->prims, c->h_prims, sizeof(DevPrim) * n_prims, hipMemcpyHostToDevice,
                          stream));
   SPT_HIP(hipMemcpyAsync(c->geo, c->h_geo, sizeof(SceneGeo), hipMemcpyHostToDevice, stream));
@@ -612,8 +714,17 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.accum = c->accum;
   K.queue = c->queue;
   K.stats = c->stats;
+  K.light_black = light_pos >= 0 && c->h_prims[p->light_id].pmax == 0.0f ? 1 : 0;
+  K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
+  K.light_pos = light_pos;
   c->n_prims = n_prims;
   c->last = K;
+  c->samples = (uint64_t)K.n_local_pix * (uint64_t)p->spp;
+  c->scene_flop = 0;
+  for (int i = 0; i < n_prims; ++i)
+    c->scene_flop += prims[i].kind == SPT_SPHERE ? SPT_FLOP_SPHERE : SPT_FLOP_RECT;
+  *c->h_kp = K;
+  SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
 
   SPT_HIP(hipMemsetAsync(c->accum, 0, sizeof(unsigned long long) * 3 * (size_t)K.n_local_pix,
                          stream));
@@ -621,7 +732,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 8, stream));
   const int grid = c->n_cu * c->blocks_per_cu;
   SPT_HIP(hipEventRecord(c->ev0, stream));
-  hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), 0, stream, K);
+  hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), 0, stream,
+                     (const KParams*)c->d_kp);
   SPT_HIP(hipGetLastError());
   SPT_HIP(hipEventRecord(c->ev1, stream));
   const uint32_t n = 3u * (uint32_t)K.n_local_pix;
@@ -641,14 +753,11 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   float ms = 0.0f;
   SPT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   std::memset(out, 0, sizeof *out);
-  out->samples = h[0]; out->path_rays = h[1]; out->shadow_rays = h[2]; out->vertices = h[3];
+  out->samples = c->samples; out->path_rays = h[1]; out->shadow_rays = h[2]; out->vertices = h[3];
   out->nee_events = h[4]; out->nee_light_hits = h[5]; out->cosine_samples = h[6];
   out->misses = h[7];
   // FLOP model (include/spt_flops.h): scene cost per ray from the primitive mix.
-  DevPrim hp[kMaxPrims];
-  SPT_HIP(hipMemcpy(hp, c->prims, sizeof(DevPrim) * c->n_prims, hipMemcpyDeviceToHost));
-  double scene = 0;
-  for (int i = 0; i < c->n_prims; ++i) scene += hp[i].kind == SPT_SPHERE ? SPT_FLOP_SPHERE : SPT_FLOP_RECT;
+  const double scene = c->scene_flop;
   out->flop = (double)out->samples * SPT_FLOP_SAMPLE +
               (double)(out->path_rays + out->shadow_rays) * scene +
               (double)out->vertices * SPT_FLOP_VERTEX +
