@@ -427,11 +427,20 @@ void spt_oracle_sincos2pi(float xi, float* s_out, float* c_out) {
 
 typedef struct {
   int kind;
-  float k, b1, b2, c1, c2; /* rect: plane k, in-plane bounds; sphere: k=rad^2 (unused), b1..: p */
-  float rad2, px, py, pz;
+  float k;                 /* rect: plane coordinate */
+  float ma, ha, mb, hb;    /* rect: in-plane bounds as |a - ma| <= ha, |b - mb| <= hb */
+  float rad2, px, py, pz;  /* sphere */
   fv e, c;
   float pmax;
 } c_prim;
+
+/* Rect bounds [lo, hi] of :106 as |a - mid| <= half with mid = (lo+hi)/2, half = (hi-lo)/2
+ * (double, rounded once to float): one subtract + one compare per axis on the GPU. Differs from
+ * the two float compares only within an ulp of an edge. Degenerate (hi < lo) rects: half = -1. */
+static void c_rect_mid(double lo, double hi, float* mid, float* half) {
+  *mid = (float)((lo + hi) * 0.5);
+  *half = hi >= lo ? (float)((hi - lo) * 0.5) : -1.0f;
+}
 
 typedef struct {
   const c_prim* prims;
@@ -476,11 +485,16 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
           continue;
         }
       }
-      /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin; for finite
-       * a, b (always, once tt < tmin) that is exactly the conjunction below. */
-      if (a >= P->b1 && a <= P->b2 && b >= P->c1 && b <= P->c2 && tt > 0.0f && tt < tmin) {
-        tmin = tt;
-        *id = i;
+      /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin:
+       * bounds as |a - mid| <= half per axis (c_rect_mid), 0 < t < tmin as one unsigned compare of the
+       * float bit patterns minus one (exact for every float incl. +-0, inf, NaN). */
+      {
+        const int inb = fabsf(a - P->ma) <= P->ha && fabsf(b - P->mb) <= P->hb;
+        const int trange = (asu(tt) - 1u) < (asu(tmin) - 1u);
+        if (inb && trange) {
+          tmin = tt;
+          *id = i;
+        }
       }
     }
   }
@@ -660,8 +674,8 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
       P->rad2 = (float)s[i].geom[0] * (float)s[i].geom[0];
       P->px = (float)s[i].geom[1]; P->py = (float)s[i].geom[2]; P->pz = (float)s[i].geom[3];
     } else {
-      P->b1 = (float)s[i].geom[0]; P->b2 = (float)s[i].geom[1];
-      P->c1 = (float)s[i].geom[2]; P->c2 = (float)s[i].geom[3];
+      c_rect_mid(s[i].geom[0], s[i].geom[1], &P->ma, &P->ha);
+      c_rect_mid(s[i].geom[2], s[i].geom[3], &P->mb, &P->hb);
       P->k = (float)s[i].geom[4];
     }
     P->e = fv3((float)s[i].e[0], (float)s[i].e[1], (float)s[i].e[2]);

@@ -46,7 +46,9 @@ static_assert(sizeof(DevPrim) == 64, "DevPrim layout");
 // Intersection geometry, grouped by kind (XY, XZ, YZ rects, then spheres; index order inside a
 // group) and read through the constant address space so every load in the intersect loop is a
 // wave-uniform s_load (scalar cache broadcast) — never a per-lane memory access.
-struct GeoRect { float k, b1, b2, c1, c2; int idx; int pad0, pad1; };   // 32 B
+// rect bounds as |a - ma| <= ha, |b - mb| <= hb (c_rect_mid in the oracle): per axis one
+// subtract + one compare, each reading a single SGPR (the VALU constant-bus limit on gfx950).
+struct GeoRect { float k, ma, ha, mb, hb; int idx; int pad0, pad1; };   // 32 B
 struct GeoSph { float px, py, pz, rad2; int idx; int pad0, pad1, pad2; };  // 32 B
 struct SceneGeo {
   int n_xy, n_xz, n_yz, n_sph;
@@ -91,18 +93,52 @@ __device__ __forceinline__ const SPT_CONST T* cptr(const T* p) {
 
 // Scene intersection of the counter-mode contract (intersect :323-335 over Rectangle_* :102-112 /
 // Sphere :229-239): grouped kind order, strict `<`, id untouched on a miss (oracle c_intersect).
-__device__ __forceinline__ void rect_group(const SPT_CONST GeoRect* g, int n, float oa, float ia,
-                                           float db, float ob, float dc, float oc, float& tmin,
-                                           int& id) {
-  for (int j = 0; j < n; ++j) {
-    int idx = g[j].idx;
-    asm volatile("" : "+s"(idx));  // keep the (uniform) index load unconditional, in an SGPR
-    const float tt = (g[j].k - oa) * ia;
-    const float a = fmaf(db, tt, ob), b = fmaf(dc, tt, oc);
-    const bool acc = (a >= g[j].b1) & (a <= g[j].b2) & (b >= g[j].c1) & (b <= g[j].c2) &
-                     (tt > 0.0f) & (tt < tmin);
-    tmin = acc ? tt : tmin;
-    id = acc ? idx : id;
+// tmin is carried as key = bits(t) - 1 so "0 < t < tmin" is ONE unsigned compare; the hit is
+// tracked as its grouped position (an inline constant when unrolled) and mapped to the primitive
+// index through LDS once per ray.
+__device__ __forceinline__ uint32_t tkey(float t) { return __float_as_uint(t) - 1u; }
+
+// Scene topology the kernel is specialised for: rect counts per kind (-1 = runtime loop), whether
+// spheres exist (runtime loop), and the light's grouped position (-1 = runtime).
+template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_>
+struct Topo {
+  static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
+  static constexpr bool SPH = SPH_;
+};
+using TopoCornell = Topo<6, 5, 6, false, 8>;     // rect[] of :287-311 (light = XZ #3 -> pos 8)
+using TopoGeneric = Topo<-1, -1, -1, true, -1>;
+
+struct Ray6 { float oa, ia, db, ob, dc, oc; };
+template <int AXIS>  // plane axis: 2 = z (XY rects), 1 = y (XZ), 0 = x (YZ)
+__device__ __forceinline__ Ray6 ray6(f3 o, f3 d, float ix, float iy, float iz) {
+  if (AXIS == 2) return Ray6{o.z, iz, d.x, o.x, d.y, o.y};
+  if (AXIS == 1) return Ray6{o.y, iy, d.x, o.x, d.z, o.z};
+  return Ray6{o.x, ix, d.y, o.y, d.z, o.z};
+}
+
+struct RectHit { float tt; bool inb; };
+__device__ __forceinline__ RectHit rect_eval(const SPT_CONST GeoRect* g, const Ray6& r) {
+  const float tt = (g->k - r.oa) * r.ia;
+  const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
+  const bool ia = fabsf(a - g->ma) <= g->ha, ib = fabsf(b - g->mb) <= g->hb;
+  return RectHit{tt, (bool)((int)ia & (int)ib)};
+}
+
+template <int N, int AXIS>  // nearest-hit over one kind group
+__device__ __forceinline__ void rect_group(const SPT_CONST GeoRect* g, int n_rt, int pos0,
+                                           const Ray6& r, uint32_t& tmin_key, int& pos) {
+  auto one = [&](const SPT_CONST GeoRect* gj, int q) {
+    const RectHit h = rect_eval(gj, r);
+    const uint32_t kk = tkey(h.tt);
+    const bool acc = h.inb & (kk < tmin_key);
+    tmin_key = acc ? kk : tmin_key;
+    pos = acc ? q : pos;
+  };
+  if constexpr (N >= 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) one(g + j, pos0 + j);
+  } else {
+    for (int j = 0; j < n_rt; ++j) one(g + j, pos0 + j);
   }
 }
 
@@ -118,35 +154,58 @@ __device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d)
   return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
 }
 
-__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, f3 o, f3 d,
-                                                float& t_out, int& id) {
+template <class TP>
+__device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; }
+
+template <class TP>
+__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, const int* pos2idx,
+                                                f3 o, f3 d, float& t_out, int& id) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
-  float tmin = 1e20f;
-  const int nxy = G->n_xy, nxz = G->n_xz, nyz = G->n_yz, nsph = G->n_sph;
-  rect_group(G->rect, nxy, o.z, iz, d.x, o.x, d.y, o.y, tmin, id);
-  rect_group(G->rect + nxy, nxz, o.y, iy, d.x, o.x, d.z, o.z, tmin, id);
-  rect_group(G->rect + nxy + nxz, nyz, o.x, ix, d.y, o.y, d.z, o.z, tmin, id);
-  for (int j = 0; j < nsph; ++j) {
-    int idx = G->sph[j].idx;
-    asm volatile("" : "+s"(idx));
-    const float ts = sphere_t(G->sph[j], o, d);
-    const bool acc = (ts != 0.0f) & (ts < tmin);
-    tmin = acc ? ts : tmin;
-    id = acc ? idx : id;
+  uint32_t tmin_key = tkey(1e20f);
+  int pos = -1;
+  const int nxy = n_of<TP>(TP::NXY, G->n_xy), nxz = n_of<TP>(TP::NXZ, G->n_xz);
+  const int nyz = n_of<TP>(TP::NYZ, G->n_yz);
+  rect_group<TP::NXY, 2>(G->rect, nxy, 0, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
+  rect_group<TP::NXZ, 1>(G->rect + nxy, nxz, nxy, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
+  rect_group<TP::NYZ, 0>(G->rect + nxy + nxz, nyz, nxy + nxz, ray6<0>(o, d, ix, iy, iz), tmin_key,
+                         pos);
+  if constexpr (TP::SPH) {
+    const int nsph = G->n_sph, base = nxy + nxz + nyz;
+    for (int j = 0; j < nsph; ++j) {
+      const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
+      const bool acc = kk < tmin_key;
+      tmin_key = acc ? kk : tmin_key;
+      pos = acc ? base + j : pos;
+    }
   }
+  const float tmin = __uint_as_float(tmin_key + 1u);
   t_out = tmin;
+  if (pos >= 0) id = pos2idx[pos];
   return tmin < 1e20f;
 }
 
-// Occluders of one rect segment [b, e) of the grouped array: accepted with t < thr.
-__device__ __forceinline__ bool occl_rects(const SPT_CONST GeoRect* g, int b, int e, float oa,
-                                           float ia, float db, float ob, float dc, float oc,
-                                           float thr, bool occ) {
-  for (int j = b; j < e; ++j) {
-    const float tt = (g[j].k - oa) * ia;
-    const float a = fmaf(db, tt, ob), c = fmaf(dc, tt, oc);
-    occ |= (a >= g[j].b1) & (a <= g[j].b2) & (c >= g[j].c1) & (c <= g[j].c2) & (tt > 0.0f) &
-           (tt < thr);
+// Occluders of one rect group: prims at grouped positions q accepted with t < tL (q > L) or
+// t <= tL (q < L); the light itself (q == L) is skipped.
+template <int N, int AXIS, int LPOS>
+__device__ __forceinline__ bool occl_group(const SPT_CONST GeoRect* g, int n_rt, int pos0, int L,
+                                           const Ray6& r, uint32_t after, bool occ) {
+  if constexpr (N >= 0 && LPOS >= 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int q = pos0 + j;  // compile-time when pos0 is
+      if (q == LPOS) continue;
+      const RectHit h = rect_eval(g + j, r);
+      const uint32_t kk = tkey(h.tt);
+      occ |= h.inb & (q < LPOS ? kk <= after : kk < after);
+    }
+  } else {
+    for (int j = 0; j < n_rt; ++j) {
+      const int q = pos0 + j;
+      if (q == L) continue;
+      const RectHit h = rect_eval(g + j, r);
+      const uint32_t kk = tkey(h.tt);
+      occ |= h.inb & ((kk < after) | ((kk == after) & (q < L)));
+    }
   }
   return occ;
 }
@@ -154,44 +213,45 @@ __device__ __forceinline__ bool occl_rects(const SPT_CONST GeoRect* g, int b, in
 // NEE shadow test for a black light: identical outcome to intersect_scene() followed by
 // `id == light` (:466-467) — the light at grouped position L wins iff it is accepted at t_L, no
 // primitive before it in grouped order is accepted with t <= t_L and none after it with t < t_L.
+template <class TP>
 __device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
                                                   const SPT_CONST SceneGeo* G, f3 o, f3 d,
                                                   float& tL) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
-  const int nxy = G->n_xy, nxz = G->n_xz, nyz = G->n_yz, nsph = G->n_sph;
-  const int lk = P->light_kind, lp = P->light_pos;
+  const int nxy = n_of<TP>(TP::NXY, G->n_xy), nxz = n_of<TP>(TP::NXZ, G->n_xz);
+  const int nyz = n_of<TP>(TP::NYZ, G->n_yz);
+  const int nrect = nxy + nxz + nyz;
+  const int lk = P->light_kind;
+  const int L = TP::LPOS >= 0 ? TP::LPOS : (lk == SPT_SPHERE ? nrect + P->light_pos : P->light_pos);
   bool ok;
-  if (lk == SPT_SPHERE) {
-    tL = sphere_t(G->sph[lp], o, d);
-    ok = (tL != 0.0f) & (tL < 1e20f);
+  if (TP::LPOS < 0 && lk == SPT_SPHERE) {
+    tL = sphere_t(G->sph[L - nrect], o, d);
+    ok = tkey(tL) < tkey(1e20f);
   } else {
-    const SPT_CONST GeoRect& R = G->rect[lp];
-    float oa, ia, db, ob, dc, oc;
-    if (lk == SPT_RECT_XY) { oa = o.z; ia = iz; db = d.x; ob = o.x; dc = d.y; oc = o.y; }
-    else if (lk == SPT_RECT_XZ) { oa = o.y; ia = iy; db = d.x; ob = o.x; dc = d.z; oc = o.z; }
-    else { oa = o.x; ia = ix; db = d.y; ob = o.y; dc = d.z; oc = o.z; }
-    tL = (R.k - oa) * ia;
-    const float a = fmaf(db, tL, ob), c = fmaf(dc, tL, oc);
-    ok = (a >= R.b1) & (a <= R.b2) & (c >= R.c1) & (c <= R.c2) & (tL > 0.0f) & (tL < 1e20f);
+    Ray6 r;
+    if (lk == SPT_RECT_XY) r = ray6<2>(o, d, ix, iy, iz);
+    else if (lk == SPT_RECT_XZ) r = ray6<1>(o, d, ix, iy, iz);
+    else r = ray6<0>(o, d, ix, iy, iz);
+    const RectHit h = rect_eval(G->rect + L, r);
+    tL = h.tt;
+    ok = h.inb & (tkey(tL) < tkey(1e20f));
   }
   if (__ballot(ok) == 0) return false;
-  const float before = __uint_as_float(__float_as_uint(tL) + 1u);  // t <= tL  <=>  t < next-up(tL)
-  const int nrect = nxy + nxz + nyz;
-  const int L = lk == SPT_SPHERE ? nrect : lp;  // rect positions < L are "before" the light
+  const uint32_t after = tkey(tL);
   bool occ = false;
-  const int e1 = nxy, e2 = nxy + nxz;
-  // XY [0,e1), XZ [e1,e2), YZ [e2,nrect): split each at the light position
-  occ = occl_rects(G->rect, 0, min(e1, L), o.z, iz, d.x, o.x, d.y, o.y, before, occ);
-  occ = occl_rects(G->rect, max(0, L + 1), e1, o.z, iz, d.x, o.x, d.y, o.y, tL, occ);
-  occ = occl_rects(G->rect, e1, min(e2, L), o.y, iy, d.x, o.x, d.z, o.z, before, occ);
-  occ = occl_rects(G->rect, max(e1, L + 1), e2, o.y, iy, d.x, o.x, d.z, o.z, tL, occ);
-  occ = occl_rects(G->rect, e2, min(nrect, L), o.x, ix, d.y, o.y, d.z, o.z, before, occ);
-  occ = occl_rects(G->rect, max(e2, L + 1), nrect, o.x, ix, d.y, o.y, d.z, o.z, tL, occ);
-  const int ls = lk == SPT_SPHERE ? lp : -1;  // sphere positions < ls are before the light
-  for (int j = 0; j < nsph; ++j) {
-    if (j == ls) continue;
-    const float ts = sphere_t(G->sph[j], o, d);
-    occ |= (ts != 0.0f) & (ts < (j < ls ? before : tL));
+  occ = occl_group<TP::NXY, 2, TP::LPOS>(G->rect, nxy, 0, L, ray6<2>(o, d, ix, iy, iz), after, occ);
+  occ = occl_group<TP::NXZ, 1, TP::LPOS>(G->rect + nxy, nxz, nxy, L, ray6<1>(o, d, ix, iy, iz),
+                                         after, occ);
+  occ = occl_group<TP::NYZ, 0, TP::LPOS>(G->rect + nxy + nxz, nyz, nxy + nxz, L,
+                                         ray6<0>(o, d, ix, iy, iz), after, occ);
+  if constexpr (TP::SPH) {
+    const int nsph = G->n_sph;
+    for (int j = 0; j < nsph; ++j) {
+      const int q = nrect + j;
+      if (q == L) continue;
+      const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
+      occ |= (kk < after) | ((kk == after) & (q < L));
+    }
   }
   return ok & !occ;
 }
@@ -201,11 +261,18 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+template <class TP>
 __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
+  __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
   {
     const SPT_CONST KParams* P = cptr(Pg);
-    for (int i = threadIdx.x; i < P->n_prims; i += kBlock) s_prims[i] = P->prims[i];
+    const SPT_CONST SceneGeo* G = cptr(P->geo);
+    const int nrect = G->n_xy + G->n_xz + G->n_yz;
+    for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
+      s_prims[i] = P->prims[i];
+      s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
+    }
   }
   __syncthreads();
 
@@ -299,7 +366,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         hit = c_hit; t = c_t; id = hit ? c_id : 0;
         carried = false;
       } else {
-        hit = intersect_scene(cptr(P->geo), o, d, t, id);
+        hit = intersect_scene<TP>(cptr(P->geo), s_pos2idx, o, d, t, id);
         ev_path = true;
       }
       const DevPrim& H = s_prims[id];
@@ -384,10 +451,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           bool to_light, sh = true;
           int ids = light_id;
           if (D->light_black) {
-            to_light = shadow_hits_light(D, cptr(D->geo), x, dl, ts);
+            to_light = shadow_hits_light<TP>(D, cptr(D->geo), x, dl, ts);
           } else {
             ids = id;
-            sh = intersect_scene(cptr(D->geo), x, dl, ts, ids);
+            sh = intersect_scene<TP>(cptr(D->geo), s_pos2idx, x, dl, ts, ids);
             to_light = ids == light_id;
           }
           ev_nee = true;
@@ -484,7 +551,8 @@ static spt_status fail(spt_status s, const std::string& msg) {
 
 struct spt_context {
   int device = 0;
-  int n_cu = 0, blocks_per_cu = 0;
+  int n_cu = 0, blocks_per_cu = 0;      // generic kernel
+  int blocks_per_cu_cornell = 0;        // TopoCornell specialisation
   DevPrim* prims = nullptr;
   SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
@@ -554,6 +622,12 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
   }
 }
 
+// Rect bounds [lo, hi] as |a - mid| <= half (contract; oracle c_rect_mid).
+static void rect_mid(double lo, double hi, float* mid, float* half) {
+  *mid = (float)((lo + hi) * 0.5);
+  *half = hi >= lo ? (float)((hi - lo) * 0.5) : -1.0f;
+}
+
 // Grouped geometry; *light_pos = position of prim `light` in rect[] / sph[] (-1 if absent).
 static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* light_pos) {
   std::memset(g, 0, sizeof *g);
@@ -566,8 +640,8 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
       if (s[i].kind != kinds[k]) continue;
       GeoRect& R = g->rect[r++];
       R.k = (float)s[i].geom[4];
-      R.b1 = (float)s[i].geom[0]; R.b2 = (float)s[i].geom[1];
-      R.c1 = (float)s[i].geom[2]; R.c2 = (float)s[i].geom[3];
+      rect_mid(s[i].geom[0], s[i].geom[1], &R.ma, &R.ha);
+      rect_mid(s[i].geom[2], s[i].geom[3], &R.mb, &R.hb);
       R.idx = i;
       if (i == light) *light_pos = r - 1;
       ++*counts[k];
@@ -601,10 +675,15 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   c->device = device;
   c->n_cu = prop.multiProcessorCount;
   int bpc = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel, kBlock, 0) != hipSuccess ||
-      bpc <= 0)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel<TopoGeneric>, kBlock, 0) !=
+          hipSuccess || bpc <= 0)
     bpc = 4;
   c->blocks_per_cu = bpc;
+  bpc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel<TopoCornell>, kBlock, 0) !=
+          hipSuccess || bpc <= 0)
+    bpc = 4;
+  c->blocks_per_cu_cornell = bpc;
   hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
   if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
@@ -730,10 +809,18 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                          stream));
   SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream));
   SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 8, stream));
-  const int grid = c->n_cu * c->blocks_per_cu;
+  // Topology specialisation: the HEAD Cornell box (6 XY, 5 XZ, 6 YZ rects, light at grouped
+  // position 8) runs a fully unrolled intersect; anything else the generic loops.
+  const SceneGeo& g = *c->h_geo;
+  const bool cornell = g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
+  const int grid = c->n_cu * (cornell ? c->blocks_per_cu_cornell : c->blocks_per_cu);
   SPT_HIP(hipEventRecord(c->ev0, stream));
-  hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), 0, stream,
-                     (const KParams*)c->d_kp);
+  if (cornell)
+    hipLaunchKernelGGL(render_kernel<TopoCornell>, dim3(grid), dim3(kBlock), 0, stream,
+                       (const KParams*)c->d_kp);
+  else
+    hipLaunchKernelGGL(render_kernel<TopoGeneric>, dim3(grid), dim3(kBlock), 0, stream,
+                       (const KParams*)c->d_kp);
   SPT_HIP(hipGetLastError());
   SPT_HIP(hipEventRecord(c->ev1, stream));
   const uint32_t n = 3u * (uint32_t)K.n_local_pix;
