@@ -356,6 +356,9 @@ void spt_oracle_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint3
 typedef struct { float x, y, z; } fv;
 static inline fv fv3(float x, float y, float z) { fv r = {x, y, z}; return r; }
 static inline float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
+static inline float u16(uint32_t lo, uint32_t hi) {
+  return (float)((lo & 0xFFu) | ((hi & 0xFFu) << 8)) * 0x1p-16f;
+}
 static inline float fdot(fv a, fv b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 /* Deterministic reciprocal / rsqrt of the contract: integer seed + 3 Newton steps (only IEEE
  * fma/mul and integer ops, so every platform computes the same bits). */
@@ -581,6 +584,10 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
     f = H->c;
     e = H->e;
     ++depth;
+    /* One Philox call per vertex: top 24 bits of r0..r3 = light x, light z, scatter xi1, xi2;
+     * the low bytes form a 16-bit RR draw (r0, r1) and a 16-bit NEE-mix draw (r2, r3). */
+    ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 0;
+    spt_oracle_philox(ctr, C->key, r);
     {
       const float p = H->pmax;
       int term = 0;
@@ -589,11 +596,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         if (!(p > 0.0f)) term = 1;
         else {
           int keep = 1;
-          if (p < 1.0f) {
-            ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 1;
-            spt_oracle_philox(ctr, C->key, r);
-            keep = u01(r[0]) < p;
-          }
+          if (p < 1.0f) keep = u16(r[0], r[1]) < p;
           if (keep) {
             const float ip = 1.0f / p;
             f = fv3(f.x * ip, f.y * ip, f.z * ip);
@@ -611,21 +614,16 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
       fv dn;
       if (P->nee_prob >= 1.0f) nee = 1;
       else if (P->nee_prob <= 0.0f) nee = 0;
-      else {
-        ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 1;
-        spt_oracle_philox(ctr, C->key, r);
-        nee = u01(r[1]) < P->nee_prob;
-      }
-      ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 0;
-      spt_oracle_philox(ctr, C->key, r);
+      else nee = u16(r[2], r[3]) < P->nee_prob;
       if (nee) {
         float xl, zl, ts;
         int ids = id, sh;
         fv dl;
         if (P->light_mode == SPT_LIGHT_GLIBC_WRAP) {
           const uint32_t dxi = (uint32_t)P->light_dx, dzi = (uint32_t)P->light_dz;
-          xl = fmaf((float)(int32_t)((r[0] >> 1) * dxi), 0x1p-31f, P->light_x0);
-          zl = fmaf((float)(int32_t)((r[1] >> 1) * dzi), 0x1p-31f, P->light_z0);
+          /* rand()*36 in int32 (:365): a 31-bit draw (top 24 bits, low 7 zero) times dx, wrapped */
+          xl = fmaf((float)(int32_t)(((r[0] >> 8) << 7) * dxi), 0x1p-31f, P->light_x0);
+          zl = fmaf((float)(int32_t)(((r[1] >> 8) << 7) * dzi), 0x1p-31f, P->light_z0);
         } else {
           xl = fmaf(u01(r[0]), P->light_dx, P->light_x0);
           zl = fmaf(u01(r[1]), P->light_dz, P->light_z0);
@@ -657,11 +655,12 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
   }
 }
 
+/* 1.31 fixed-point per-sample contribution: min(L/spp, 1) * 2^31 truncated, negatives -> 0
+ * (fminf(NaN, 1) = 1). Integer sums are order-independent: results never depend on the GPU's
+ * unit size, lane or queue order, or the GPU count. */
 static inline uint64_t c_fix(float L, float inv_spp) {
-  float c = L * inv_spp;
-  if (!(c >= 0.0f)) c = 0.0f;
-  if (c > 1.0f) c = 1.0f;
-  return (uint64_t)(c * 4294967296.0f);
+  const float v = fminf(L * inv_spp, 1.0f) * 2147483648.0f;
+  return v >= 0.0f ? (uint64_t)(uint32_t)v : 0u;
 }
 
 static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
@@ -729,7 +728,7 @@ int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* ca
           acc[2] += c_fix(L.z, inv_spp);
         }
         for (ch = 0; ch < 3; ch++) {
-          float v = (float)acc[ch] * 0x1p-32f;
+          float v = (float)acc[ch] * 0x1p-31f;
           rgb_out[((size_t)ri * (size_t)P->width + (size_t)x) * 3 + (size_t)ch] = v > 1.0f ? 1.0f : v;
         }
       }

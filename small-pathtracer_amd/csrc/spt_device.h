@@ -41,6 +41,10 @@ __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
 }
 
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
+// 16-bit draw from the low bytes of two Philox words (RR and NEE-mix draws, see the kernel).
+__device__ __forceinline__ float u16(uint32_t lo, uint32_t hi) {
+  return (float)((lo & 0xFFu) | ((hi & 0xFFu) << 8)) * 0x1p-16f;
+}
 
 // ---- deterministic reciprocal / reciprocal square root (contract): integer seed + 3 Newton
 // steps; max relative error 6e-8 / 1.3e-7 (oracle tests). rcp_nr(+-0) is NaN, which the
@@ -119,12 +123,11 @@ __device__ __forceinline__ f3 cosine_dir(f3 nl, uint32_t ra, uint32_t rb) {
                        fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr))));
 }
 
-// Fixed-point per-sample contribution (order-independent, exact integer accumulation).
-__device__ __forceinline__ unsigned long long fix32(float L, float inv_spp) {
-  float c = L * inv_spp;
-  if (!(c >= 0.0f)) c = 0.0f;
-  if (c > 1.0f) c = 1.0f;
-  return (unsigned long long)(c * 4294967296.0f);
+// 1.31 fixed-point per-sample contribution (order-independent, exact integer accumulation):
+// min(L/spp, 1) * 2^31 truncated; v_cvt_u32_f32 saturates negatives to 0.
+__device__ __forceinline__ uint32_t fix31(float L, float inv_spp) {
+  const float v = fminf(L * inv_spp, 1.0f) * 2147483648.0f;
+  return v >= 0.0f ? (uint32_t)v : 0u;
 }
 
 }  // namespace spt

@@ -394,6 +394,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       const f3 e = mk(H.ex, H.ey, H.ez);
       const float p = H.pmax;
       ++depth;
+      // One Philox call per vertex: top 24 bits of r.x..r.w = light x, light z, scatter xi1, xi2;
+      // low bytes = a 16-bit RR draw (r.x, r.y) and a 16-bit NEE-mix draw (r.z, r.w).
+      const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 0u, cptr(Pg)->key0, cptr(Pg)->key1);
       // Russian roulette :448-454 (+ optional hard depth cap).
       bool term = false;
       const int max_depth = P->max_depth;
@@ -404,11 +407,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           term = true;
         } else {
           bool keep = true;
-          if (p < 1.0f) {
-            const SPT_CONST KParams* C = cptr(Pg);
-            const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, C->key0, C->key1);
-            keep = u01(r.x) < p;
-          }
+          if (p < 1.0f) keep = u16(r.x, r.y) < p;
           if (keep) {
             const float ip = 1.0f / p;
             f = mk(f.x * ip, f.y * ip, f.z * ip);
@@ -424,11 +423,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const float q = C->nee_prob;
         if (q >= 1.0f) nee = true;
         else if (q <= 0.0f) nee = false;
-        else {
-          const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 1u, C->key0, C->key1);
-          nee = u01(r.y) < q;
-        }
-        const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 0u, C->key0, C->key1);
+        else nee = u16(r.z, r.w) < q;
         float w = 1.0f;
         f3 dn;
         bool light_end = false;
@@ -439,8 +434,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           const SPT_CONST KParams* D = cptr(Pg);
           float xl, zl;
           if (D->light_mode == SPT_LIGHT_GLIBC_WRAP) {
-            xl = fmaf((float)(int32_t)((r.x >> 1) * D->ldxi), 0x1p-31f, D->lx0);
-            zl = fmaf((float)(int32_t)((r.y >> 1) * D->ldzi), 0x1p-31f, D->lz0);
+            xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * D->ldxi), 0x1p-31f, D->lx0);
+            zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * D->ldzi), 0x1p-31f, D->lz0);
           } else {
             xl = fmaf(u01(r.x), D->ldx, D->lx0);
             zl = fmaf(u01(r.y), D->ldz, D->lz0);
@@ -493,9 +488,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       }
       if (term) {
         const float inv_spp = cptr(Pg)->inv_spp;
-        acc0 += fix32(L.x, inv_spp);
-        acc1 += fix32(L.y, inv_spp);
-        acc2 += fix32(L.z, inv_spp);
+        acc0 += fix31(L.x, inv_spp);
+        acc1 += fix31(L.y, inv_spp);
+        acc2 += fix31(L.z, inv_spp);
         ++s;
         need_cam = true;
       }
@@ -519,12 +514,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   }
 }
 
-// 32.32 fixed point -> float, clamp :538 (values are >= 0 by construction).
+// 1.31 fixed point -> float, clamp :538 (values are >= 0 by construction).
 __global__ void __launch_bounds__(kBlock)
 finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict__ rgb, uint32_t n) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i < n) {
-    const float v = (float)accum[i] * 0x1p-32f;
+    const float v = (float)accum[i] * 0x1p-31f;
     rgb[i] = v > 1.0f ? 1.0f : v;
   }
 }
