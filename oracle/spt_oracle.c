@@ -532,15 +532,18 @@ typedef struct {
 static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const float cam[12],
                  c_stats* st) {
   const spt_params* P = C->P;
-  uint32_t ctr[4], r[4];
+  uint32_t ctr[4], r[4], rl[4];
   fv o, d, T = fv3(1, 1, 1), L = fv3(0, 0, 0);
   int depth = 0, carried = 0, c_hit = 0, c_id = 0;
   float c_t = 0;
-  ctr[0] = pix; ctr[1] = s; ctr[2] = 0; ctr[3] = 0;
+  /* Camera ray :533-536. The jitter comes from the low bytes of vertex 1's Philox call (16 bits
+   * each), so a sample start costs no extra RNG call; 1/w, 1/h are rounded once. */
+  ctr[0] = pix; ctr[1] = s; ctr[2] = 1; ctr[3] = 0;
   spt_oracle_philox(ctr, C->key, r);
   {
-    const float su = (((float)px - 0.5f) + u01(r[0])) / (float)P->width;
-    const float sv = (((float)(P->height - py - 1) - 0.5f) + u01(r[1])) / (float)P->height;
+    const float inv_w = 1.0f / (float)P->width, inv_h = 1.0f / (float)P->height;
+    const float su = (((float)px - 0.5f) + u16(r[0], r[1])) * inv_w;
+    const float sv = (((float)(P->height - py - 1) - 0.5f) + u16(r[2], r[3])) * inv_h;
     o = fv3(cam[0], cam[1], cam[2]);
     d = fnormalize(fv3(fmaf(cam[9], sv, fmaf(cam[6], su, cam[3])) - cam[0],
                        fmaf(cam[10], sv, fmaf(cam[7], su, cam[4])) - cam[1],
@@ -585,9 +588,16 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
     e = H->e;
     ++depth;
     /* One Philox call per vertex: top 24 bits of r0..r3 = light x, light z, scatter xi1, xi2;
-     * the low bytes form a 16-bit RR draw (r0, r1) and a 16-bit NEE-mix draw (r2, r3). */
+     * the low bytes form a 16-bit RR draw (r0, r1) and a 16-bit NEE-mix draw (r2, r3) — except at
+     * vertex 1, whose low bytes were the camera jitter: its RR / NEE-mix draws (only needed when
+     * rr_depth < 1 or 0 < nee_prob < 1) come from stream 1. */
     ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 0;
     spt_oracle_philox(ctr, C->key, r);
+    rl[0] = r[0]; rl[1] = r[1]; rl[2] = r[2]; rl[3] = r[3];
+    if (depth == 1) {
+      ctr[3] = 1;
+      spt_oracle_philox(ctr, C->key, rl);
+    }
     {
       const float p = H->pmax;
       int term = 0;
@@ -596,7 +606,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         if (!(p > 0.0f)) term = 1;
         else {
           int keep = 1;
-          if (p < 1.0f) keep = u16(r[0], r[1]) < p;
+          if (p < 1.0f) keep = u16(rl[0], rl[1]) < p;
           if (keep) {
             const float ip = 1.0f / p;
             f = fv3(f.x * ip, f.y * ip, f.z * ip);
@@ -614,7 +624,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
       fv dn;
       if (P->nee_prob >= 1.0f) nee = 1;
       else if (P->nee_prob <= 0.0f) nee = 0;
-      else nee = u16(r[2], r[3]) < P->nee_prob;
+      else nee = u16(rl[2], rl[3]) < P->nee_prob;
       if (nee) {
         float xl, zl, ts;
         int ids = id, sh;

@@ -27,7 +27,8 @@ from typing import Iterable, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspt.so")
+# SPT_LIB overrides the library (A/B builds in tools/ab.sh); the default is the in-tree build.
+LIB_PATH = os.environ.get("SPT_LIB") or os.path.join(_HERE, "libspt.so")
 
 DIFF, SPEC, REFR = 0, 1, 2
 RECT_XY, RECT_XZ, RECT_YZ, SPHERE = 0, 1, 2, 3

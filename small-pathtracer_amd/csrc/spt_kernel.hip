@@ -73,7 +73,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   int tile_rows, shard_index, shard_count;
   int chunk, n_local_pix;
   uint32_t n_units;
-  float inv_spp;
+  float inv_spp, inv_w, inv_h;
   // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
   // always ends there (RR with p == 0, :448), so the NEE test only needs "is the nearest hit the
   // light" — an occlusion query without id bookkeeping.
@@ -342,12 +342,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
          ev_cos = false;
     const bool ev_vert = has_unit;
     if (has_unit) {
+      // One Philox call per lane per iteration, for the vertex about to be shaded: top 24 bits of
+      // r.x..r.w = light x, light z, scatter xi1, xi2; low bytes = RR draw (r.x, r.y) and NEE-mix
+      // draw (r.z, r.w) — at vertex 1 the low bytes are the camera jitter instead.
+      const u4 r = philox4x32_10(pix, s, need_cam ? 1u : (uint32_t)depth + 1u, 0u,
+                                 cptr(Pg)->key0, cptr(Pg)->key1);
       // 3) camera ray for lanes starting a sample (:533-536).
       if (need_cam) {
         const SPT_CONST KParams* C = cptr(Pg);
-        const u4 r = philox4x32_10(pix, s, 0u, 0u, C->key0, C->key1);
-        const float su = (((float)px - 0.5f) + u01(r.x)) / (float)C->width;
-        const float sv = (((float)(C->height - py - 1) - 0.5f) + u01(r.y)) / (float)C->height;
+        const float su = (((float)px - 0.5f) + u16(r.x, r.y)) * C->inv_w;
+        const float sv = (((float)(C->height - py - 1) - 0.5f) + u16(r.z, r.w)) * C->inv_h;
         o = mk(C->cam[0], C->cam[1], C->cam[2]);
         d = normalize3(mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
                           fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
@@ -394,9 +398,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       const f3 e = mk(H.ex, H.ey, H.ez);
       const float p = H.pmax;
       ++depth;
-      // One Philox call per vertex: top 24 bits of r.x..r.w = light x, light z, scatter xi1, xi2;
-      // low bytes = a 16-bit RR draw (r.x, r.y) and a 16-bit NEE-mix draw (r.z, r.w).
-      const u4 r = philox4x32_10(pix, s, (uint32_t)depth, 0u, cptr(Pg)->key0, cptr(Pg)->key1);
+      u4 rl = r;  // RR / NEE-mix draws; at vertex 1 from stream 1 (only configs that need them)
+      if (depth == 1) {
+        const SPT_CONST KParams* C = cptr(Pg);
+        if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
+          rl = philox4x32_10(pix, s, 1u, 1u, C->key0, C->key1);
+      }
       // Russian roulette :448-454 (+ optional hard depth cap).
       bool term = false;
       const int max_depth = P->max_depth;
@@ -407,7 +414,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           term = true;
         } else {
           bool keep = true;
-          if (p < 1.0f) keep = u16(r.x, r.y) < p;
+          if (p < 1.0f) keep = u16(rl.x, rl.y) < p;
           if (keep) {
             const float ip = 1.0f / p;
             f = mk(f.x * ip, f.y * ip, f.z * ip);
@@ -423,7 +430,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const float q = C->nee_prob;
         if (q >= 1.0f) nee = true;
         else if (q <= 0.0f) nee = false;
-        else nee = u16(r.z, r.w) < q;
+        else nee = u16(rl.z, rl.w) < q;
         float w = 1.0f;
         f3 dn;
         bool light_end = false;
@@ -785,6 +792,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   if (n_units >= 0xFFFF0000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
   K.inv_spp = 1.0f / (float)p->spp;
+  K.inv_w = 1.0f / (float)p->width;
+  K.inv_h = 1.0f / (float)p->height;
   K.accum = c->accum;
   K.queue = c->queue;
   K.stats = c->stats;
