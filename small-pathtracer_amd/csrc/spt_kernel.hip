@@ -32,6 +32,7 @@ namespace spt {
 constexpr int kMaxPrims = 64;
 constexpr int kBlock = 256;
 constexpr uint32_t kGrab = 64;  // units fetched per queue atomic
+constexpr int kStatWords = 32;   // [0,8) path stats, [8,28) region stats (diagnostic build)
 
 // 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
 // axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
@@ -256,6 +257,22 @@ __device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
   return ok & !occ;
 }
 
+// Diagnostic build (-DSPT_REGION_STATS): per code region, wave executions and active lanes,
+// counted with wave-uniform SALU ballots and flushed once per wave to stats[8 + 2*region].
+#ifdef SPT_REGION_STATS
+constexpr int kRegions = 10;
+#define SPT_REGION(R)                                                   \
+  do {                                                                  \
+    const uint64_t m_ = __ballot(1);                                    \
+    reg_exec[R] += 1u;                                                  \
+    reg_lanes[R] += (uint32_t)__popcll(m_);                             \
+  } while (0)
+#else
+#define SPT_REGION(R) \
+  do {                \
+  } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -288,11 +305,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   uint32_t pool_next = 0, pool_end = 0;
   bool exhausted = false;
   uint32_t n_path = 0, n_shadow = 0, n_vert = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
+#ifdef SPT_REGION_STATS
+  uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
+#endif
 
   for (;;) {
     const SPT_CONST KParams* P = cptr(Pg);
     // 1) retire finished units: flush the fixed-point sums of their pixel.
+    SPT_REGION(0);  // loop iteration
     if (has_unit && need_cam && s >= s_end) {
+      SPT_REGION(1);  // unit retire
       unsigned long long* a = P->accum + 3ull * lp;
       if (acc0) atomicAdd(a + 0, acc0);
       if (acc1) atomicAdd(a + 1, acc1);
@@ -304,6 +326,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     bool needs_unit = !has_unit;
     uint64_t need = __ballot(needs_unit);
     while (need != 0 && !exhausted) {
+      SPT_REGION(2);  // refill
       const SPT_CONST KParams* Q = cptr(Pg);
       if (pool_next >= pool_end) {
         uint32_t b = 0;
@@ -349,6 +372,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
                                  cptr(Pg)->key0, cptr(Pg)->key1);
       // 3) camera ray for lanes starting a sample (:533-536).
       if (need_cam) {
+        SPT_REGION(3);  // camera ray
         const SPT_CONST KParams* C = cptr(Pg);
         const float su = (((float)px - 0.5f) + u16(r.x, r.y)) * C->inv_w;
         const float sv = (((float)(C->height - py - 1) - 0.5f) + u16(r.z, r.w)) * C->inv_h;
@@ -370,6 +394,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         hit = c_hit; t = c_t; id = hit ? c_id : 0;
         carried = false;
       } else {
+        SPT_REGION(4);  // path-ray intersect
         hit = intersect_scene<TP>(cptr(P->geo), s_pos2idx, o, d, t, id);
         ev_path = true;
       }
@@ -424,6 +449,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         }
       }
       if (!term) {
+        SPT_REGION(5);  // DIFF shading (continuing vertex)
         // DIFF :457-480.
         const SPT_CONST KParams* C = cptr(Pg);
         bool nee;
@@ -453,6 +479,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           bool to_light, sh = true;
           int ids = light_id;
           if (D->light_black) {
+            SPT_REGION(6);  // shadow test
             to_light = shadow_hits_light<TP>(D, cptr(D->geo), x, dl, ts);
           } else {
             ids = id;
@@ -461,6 +488,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           }
           ev_nee = true;
           if (to_light) {
+            SPT_REGION(7);  // NEE light hit
             ev_nee_hit = true;
             const float pdf = fabsf((cptr(Pg)->larea * dl.y) / (ts * ts));
             const float brdf = fabsf(dot3(dl, nl) * 0.318309886183790672f);
@@ -478,6 +506,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           }
         }
         if (scatter) {
+          SPT_REGION(8);  // cosine direction
           dn = cosine_dir(nl, r.z, r.w);
           ev_cos = true;
         }
@@ -494,6 +523,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
       }
       if (term) {
+        SPT_REGION(9);  // path end: accumulate
         const float inv_spp = cptr(Pg)->inv_spp;
         acc0 += fix31(L.x, inv_spp);
         acc1 += fix31(L.y, inv_spp);
@@ -511,6 +541,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   }
   if (lane == 0) {
     unsigned long long* st = cptr(Pg)->stats;
+#ifdef SPT_REGION_STATS
+    for (int r = 0; r < kRegions; ++r) {
+      atomicAdd(st + 8 + 2 * r, (unsigned long long)reg_exec[r]);
+      atomicAdd(st + 9 + 2 * r, (unsigned long long)reg_lanes[r]);
+    }
+#endif
     atomicAdd(st + 1, (unsigned long long)n_path);
     atomicAdd(st + 2, (unsigned long long)n_shadow);
     atomicAdd(st + 3, (unsigned long long)n_vert);
@@ -693,7 +729,7 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_kp, sizeof(KParams));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_kp, sizeof(KParams), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(&c->queue, sizeof(uint32_t) * 64);
-  if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * 8);
+  if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * kStatWords);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e != hipSuccess) {
@@ -812,7 +848,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   SPT_HIP(hipMemsetAsync(c->accum, 0, sizeof(unsigned long long) * 3 * (size_t)K.n_local_pix,
                          stream));
   SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream));
-  SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * 8, stream));
+  SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
   // Topology specialisation: the HEAD Cornell box (6 XY, 5 XZ, 6 YZ rects, light at grouped
   // position 8) runs a fully unrolled intersect; anything else the generic loops.
   const SceneGeo& g = *c->h_geo;
@@ -839,8 +875,19 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   if (!c || !out) return fail(SPT_ERR_INVALID_ARG, "null argument");
   SPT_HIP(hipSetDevice(c->device));
   SPT_HIP(hipEventSynchronize(c->ev1));
-  unsigned long long h[8];
+  unsigned long long h[kStatWords];
   SPT_HIP(hipMemcpy(h, c->stats, sizeof h, hipMemcpyDeviceToHost));
+#ifdef SPT_REGION_STATS
+  {
+    static const char* names[10] = {"iteration", "unit_retire", "refill", "camera", "path_isect",
+                                    "diff_shading", "shadow_test", "nee_light_hit", "cosine",
+                                    "path_end"};
+    std::fprintf(stderr, "SPT_REGION_STATS");
+    for (int r = 0; r < 10; ++r)
+      std::fprintf(stderr, " %s=%llu/%llu", names[r], h[8 + 2 * r], h[9 + 2 * r]);
+    std::fprintf(stderr, "\n");
+  }
+#endif
   float ms = 0.0f;
   SPT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   std::memset(out, 0, sizeof *out);
