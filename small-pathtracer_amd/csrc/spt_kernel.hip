@@ -261,12 +261,7 @@ __device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
 // counted with wave-uniform SALU ballots and flushed once per wave to stats[8 + 2*region].
 #ifdef SPT_REGION_STATS
 constexpr int kRegions = 10;
-#define SPT_REGION(R)                                                   \
-  do {                                                                  \
-    const uint64_t m_ = __ballot(1);                                    \
-    reg_exec[R] += 1u;                                                  \
-    reg_lanes[R] += (uint32_t)__popcll(m_);                             \
-  } while (0)
+#define SPT_REGION(R) (reg_flags |= 1u << (R))  // per lane; ballot-counted at the loop end
 #else
 #define SPT_REGION(R) \
   do {                \
@@ -307,6 +302,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   uint32_t n_path = 0, n_shadow = 0, n_vert = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
+  uint32_t reg_flags = 0;
 #endif
 
   for (;;) {
@@ -538,6 +534,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     n_shadow += (uint32_t)__popcll(__ballot(ev_nee));
     n_nee_hit += (uint32_t)__popcll(__ballot(ev_nee_hit));
     n_cos += (uint32_t)__popcll(__ballot(ev_cos));
+#ifdef SPT_REGION_STATS
+#pragma unroll
+    for (int r = 0; r < kRegions; ++r) {
+      const uint64_t m = __ballot((reg_flags >> r) & 1u);
+      reg_exec[r] += m != 0;
+      reg_lanes[r] += (uint32_t)__popcll(m);
+    }
+    reg_flags = 0;
+#endif
   }
   if (lane == 0) {
     unsigned long long* st = cptr(Pg)->stats;
