@@ -77,7 +77,7 @@ typedef enum spt_light_mode { SPT_LIGHT_GLIBC_WRAP = 0, SPT_LIGHT_UNIFORM = 1 } 
 
 typedef struct spt_params {
   int32_t width, height, spp; /* :507-508 */
-  uint32_t seed;              /* Philox4x32-10 key word 0 (key word 1 = SPT_PHILOX_KEY1) */
+  uint32_t seed;              /* Philox4x32-10 counter word 3 (the key is the fixed SPT_PHILOX_KEY) */
   float nee_prob;             /* Q of :464 (`q < Q`): 1 = HEAD explicit light sampling, 0 = cosine only */
   int32_t rr_depth;           /* Russian roulette starts when ++depth > rr_depth  (:448, HEAD = 5) */
   int32_t max_depth;          /* 0 = unbounded (reference); >0 = path ends at this vertex depth */
@@ -96,6 +96,9 @@ typedef struct spt_params {
   uint32_t flags;             /* reserved, must be 0 */
 } spt_params;
 
+/* Philox4x32-10 key (fixed, so the key schedule is compile-time) and counter layout:
+ * ctr = (pixel = y*w + x, sample, vertex | stream << 31, seed). */
+#define SPT_PHILOX_KEY0 0x53505430u /* "SPT0" */
 #define SPT_PHILOX_KEY1 0x53505431u /* "SPT1" */
 
 /* Per-render path statistics (counted in-kernel, summed once per wave). */

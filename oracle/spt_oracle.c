@@ -14,7 +14,8 @@
  *     (pinned against oracle/_ref in tests/test_oracle_golden.py and tests/golden/).
  *
  *  2. COUNTER mode (spt_oracle_counter_render): the device path's contract — the same algorithm in
- *     fp32 with a counter-based Philox4x32-10 stream keyed by (seed; pixel, sample, vertex, stream),
+ *     fp32 with a counter-based Philox4x32-10 stream (fixed key; counter = pixel, sample,
+ *     vertex | stream << 31, seed),
  *     an iterative bounce loop and fixed-point per-pixel accumulation. Every float operation is
  *     spelled out (explicit fmaf, correctly rounded div/sqrt, own sincos polynomial) so that the HIP
  *     kernel must reproduce it BIT-EXACTLY. See DESIGN.md "Counter-mode contract".
@@ -538,7 +539,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
   float c_t = 0;
   /* Camera ray :533-536. The jitter comes from the low bytes of vertex 1's Philox call (16 bits
    * each), so a sample start costs no extra RNG call; 1/w, 1/h are rounded once. */
-  ctr[0] = pix; ctr[1] = s; ctr[2] = 1; ctr[3] = 0;
+  ctr[0] = pix; ctr[1] = s; ctr[2] = 1; ctr[3] = P->seed;
   spt_oracle_philox(ctr, C->key, r);
   {
     const float inv_w = 1.0f / (float)P->width, inv_h = 1.0f / (float)P->height;
@@ -591,11 +592,11 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
      * the low bytes form a 16-bit RR draw (r0, r1) and a 16-bit NEE-mix draw (r2, r3) — except at
      * vertex 1, whose low bytes were the camera jitter: its RR / NEE-mix draws (only needed when
      * rr_depth < 1 or 0 < nee_prob < 1) come from stream 1. */
-    ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = 0;
+    ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = P->seed;
     spt_oracle_philox(ctr, C->key, r);
     rl[0] = r[0]; rl[1] = r[1]; rl[2] = r[2]; rl[3] = r[3];
     if (depth == 1) {
-      ctr[3] = 1;
+      ctr[2] = 1u | 0x80000000u; /* stream 1 */
       spt_oracle_philox(ctr, C->key, rl);
     }
     {
@@ -707,7 +708,7 @@ int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* ca
   int i, ri;
   memset(&tot, 0, sizeof tot);
   c_prims_from_spt(prims, n, CP);
-  C.prims = CP; C.n = n; C.P = P; C.key[0] = P->seed; C.key[1] = SPT_PHILOX_KEY1;
+  C.prims = CP; C.n = n; C.P = P; C.key[0] = SPT_PHILOX_KEY0; C.key[1] = SPT_PHILOX_KEY1;
   for (i = 0; i < 3; i++) {
     camf[i] = (float)cam->origin[i];
     camf[3 + i] = (float)cam->lower_left_corner[i];

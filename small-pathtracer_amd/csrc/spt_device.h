@@ -14,20 +14,21 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/spt.h"
+
 namespace spt {
 
 // ---- Philox4x32-10 (Salmon et al. SC'11), replaces erand48/rand() (utilities.h:26-51,
-// smallpt.cpp:365-366,460,533-534). Counter = (pixel, sample, vertex, stream), key = (seed, "SPT1").
+// smallpt.cpp:365-366,460,533-534). Fixed key (SPT_PHILOX_KEY0/1): the whole key schedule is
+// compile-time, so each round is two v_mad_u64_u32 and four v_xor_b32 with literal/VGPR operands
+// and no SALU. Counter = (pixel, sample, vertex | stream << 31, seed).
 constexpr uint32_t kPhM0 = 0xD2511F53u, kPhM1 = 0xCD9E8D57u;
 constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
 
 struct u4 { uint32_t x, y, z, w; };
 
-__device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                            uint32_t k0, uint32_t k1) {
-  // Keep the key opaque so the (wave-uniform) key schedule is recomputed with SALU adds per call
-  // instead of being hoisted into 20 live SGPRs.
-  asm volatile("" : "+s"(k0), "+s"(k1));
+__device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  uint32_t k0 = SPT_PHILOX_KEY0, k1 = SPT_PHILOX_KEY1;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)kPhM0 * c0;  // one v_mad_u64_u32 each (hi and lo together)

@@ -65,7 +65,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   int n_prims;
   float cam[12];  // origin, lower_left_corner, horizontal, vertical
   int width, height, spp;
-  uint32_t key0, key1;
+  uint32_t seed;
   float nee_prob;
   int rr_depth, max_depth, light_id;
   float lx0, ldx, lz0, ldz, ly, larea;
@@ -299,6 +299,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   // ---- wave-uniform state
   uint32_t pool_next = 0, pool_end = 0;
   bool exhausted = false;
+  // per-lane event counters (VALU adds under the event's own exec mask; reduced once per wave)
   uint32_t n_path = 0, n_shadow = 0, n_vert = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
@@ -356,16 +357,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     }
     if (__ballot(has_unit) == 0) break;
 
-    // per-lane events of this iteration, counted by ballots at the convergent end of the loop
-    bool ev_path = false, ev_miss = false, ev_vert2 = false, ev_nee = false, ev_nee_hit = false,
-         ev_cos = false;
-    const bool ev_vert = has_unit;
     if (has_unit) {
+      ++n_vert;
       // One Philox call per lane per iteration, for the vertex about to be shaded: top 24 bits of
       // r.x..r.w = light x, light z, scatter xi1, xi2; low bytes = RR draw (r.x, r.y) and NEE-mix
       // draw (r.z, r.w) — at vertex 1 the low bytes are the camera jitter instead.
-      const u4 r = philox4x32_10(pix, s, need_cam ? 1u : (uint32_t)depth + 1u, 0u,
-                                 cptr(Pg)->key0, cptr(Pg)->key1);
+      const u4 r = philox4x32_10(pix, s, need_cam ? 1u : (uint32_t)depth + 1u, cptr(Pg)->seed);
       // 3) camera ray for lanes starting a sample (:533-536).
       if (need_cam) {
         SPT_REGION(3);  // camera ray
@@ -392,14 +389,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       } else {
         SPT_REGION(4);  // path-ray intersect
         hit = intersect_scene<TP>(cptr(P->geo), s_pos2idx, o, d, t, id);
-        ev_path = true;
+        ++n_path;
       }
       const DevPrim& H = s_prims[id];
       const int kind = H.kind;
       f3 x;
       if (!hit) {
         x = mk(0, 0, 0);
-        ev_miss = true;
+        ++n_miss;
       } else {
         float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
         if (kind == SPT_RECT_XY) tr = (H.w1 - o.z) / d.z;
@@ -423,7 +420,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       if (depth == 1) {
         const SPT_CONST KParams* C = cptr(Pg);
         if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
-          rl = philox4x32_10(pix, s, 1u, 1u, C->key0, C->key1);
+          rl = philox4x32_10(pix, s, 1u | 0x80000000u, C->seed);
       }
       // Russian roulette :448-454 (+ optional hard depth cap).
       bool term = false;
@@ -482,10 +479,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
             sh = intersect_scene<TP>(cptr(D->geo), s_pos2idx, x, dl, ts, ids);
             to_light = ids == light_id;
           }
-          ev_nee = true;
+          ++n_shadow;
           if (to_light) {
             SPT_REGION(7);  // NEE light hit
-            ev_nee_hit = true;
+            ++n_nee_hit;
             const float pdf = fabsf((cptr(Pg)->larea * dl.y) / (ts * ts));
             const float brdf = fabsf(dot3(dl, nl) * 0.318309886183790672f);
             w = pdf * brdf;
@@ -504,14 +501,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         if (scatter) {
           SPT_REGION(8);  // cosine direction
           dn = cosine_dir(nl, r.z, r.w);
-          ev_cos = true;
+          ++n_cos;
         }
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
         T = mk((T.x * f.x) * w, (T.y * f.y) * w, (T.z * f.z) * w);
         o = x;
         d = dn;
         if (light_end) {
-          ev_vert2 = true;
+          ++n_vert;
           L = mk(fmaf(T.x, e_light.x, L.x), fmaf(T.y, e_light.y, L.y), fmaf(T.z, e_light.z, L.z));
           term = true;
         }
@@ -528,12 +525,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         need_cam = true;
       }
     }
-    n_path += (uint32_t)__popcll(__ballot(ev_path));
-    n_miss += (uint32_t)__popcll(__ballot(ev_miss));
-    n_vert += (uint32_t)__popcll(__ballot(ev_vert)) + (uint32_t)__popcll(__ballot(ev_vert2));
-    n_shadow += (uint32_t)__popcll(__ballot(ev_nee));
-    n_nee_hit += (uint32_t)__popcll(__ballot(ev_nee_hit));
-    n_cos += (uint32_t)__popcll(__ballot(ev_cos));
 #ifdef SPT_REGION_STATS
 #pragma unroll
     for (int r = 0; r < kRegions; ++r) {
@@ -544,12 +535,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     reg_flags = 0;
 #endif
   }
-  if (lane == 0) {
-    unsigned long long* st = cptr(Pg)->stats;
+  {
+    unsigned long long* st = cptr(Pg)->stats;  // wave-reduced by the atomic optimizer
 #ifdef SPT_REGION_STATS
-    for (int r = 0; r < kRegions; ++r) {
-      atomicAdd(st + 8 + 2 * r, (unsigned long long)reg_exec[r]);
-      atomicAdd(st + 9 + 2 * r, (unsigned long long)reg_lanes[r]);
+    if (lane == 0) {  // wave-uniform values: one lane adds them
+      for (int r = 0; r < kRegions; ++r) {
+        atomicAdd(st + 8 + 2 * r, (unsigned long long)reg_exec[r]);
+        atomicAdd(st + 9 + 2 * r, (unsigned long long)reg_lanes[r]);
+      }
     }
 #endif
     atomicAdd(st + 1, (unsigned long long)n_path);
@@ -807,7 +800,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     K.cam[9 + i] = (float)cam->vertical[i];
   }
   K.width = p->width; K.height = p->height; K.spp = p->spp;
-  K.key0 = p->seed; K.key1 = SPT_PHILOX_KEY1;
+  K.seed = p->seed;
   K.nee_prob = p->nee_prob; K.rr_depth = p->rr_depth; K.max_depth = p->max_depth;
   K.light_id = p->light_id;
   K.lx0 = p->light_x0; K.ldx = p->light_dx; K.lz0 = p->light_z0; K.ldz = p->light_dz;

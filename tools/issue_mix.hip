@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(256) k(float* out, float seed, int n) {
         asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a3) : "v"(a0), "v"(a1));
       }
 #pragma unroll
-      for (int j = 0; j < S; ++j) asm volatile("s_and_b64 s[20:21], s[20:21], s[22:23]" ::: "s20", "s21");
+      for (int j = 0; j < S; ++j) asm volatile("s_and_b64 s[20:21], s[20:21], s[22:23]" ::: "s20", "s21", "scc");
     }
   }
   out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + t + (float)pos;
