@@ -61,8 +61,7 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
     oracle.counter_render(prims, cam._c, params, rows=calib, threads=threads)
     t_row = max(time.perf_counter() - t0, 1e-3) / len(calib)
     n_rows = int(max(1, min(h, round(budget_s / t_row))))
-    stride = max(1, h // n_rows)
-    rows = np.arange(stride // 2, h, stride, dtype=np.int32)[:n_rows]
+    rows = np.unique(np.linspace(0, h - 1, n_rows).round().astype(np.int32))  # cyclic spread
     t0 = time.perf_counter()
     img, st = oracle.counter_render(prims, cam._c, params, rows=rows, threads=threads)
     dt = time.perf_counter() - t0
@@ -70,7 +69,7 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
     exact = gpu_img is not None and np.array_equal(gpu_img[rows], img)
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
             "kind": "port",
-            "sample": f"{len(rows)} of {h} rows (every {stride}th), {w}x{spp} spp each = "
+            "sample": f"{len(rows)} of {h} rows evenly spread, {w}x{spp} spp each = "
                       f"{samples} samples in {dt:.1f} s; oracle/spt_oracle.c counter mode, "
                       f"OpenMP dynamic rows",
             "gpu_rows_bit_exact": bool(exact)}
@@ -104,6 +103,7 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     spt = importlib.import_module("small-pathtracer_amd")
+    sd = importlib.import_module("small-pathtracer_amd.distributed")
     cfg = dict(CONFIGS[args.config])
     scaling = args.scaling or cfg["scaling"]
     spp = args.spp or cfg["spp"]
@@ -115,10 +115,10 @@ def main() -> None:
     params = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
                                 max_depth=cfg["max_depth"], tile_rows=8, shard_index=rank,
                                 shard_count=world, device=local)
-    rows_of = [spt.shard_rows(spt.default_params(height=h, tile_rows=8, shard_index=k,
-                                                 shard_count=world)) for k in range(world)]
+    rows_of = sd.shard_row_lists(h, 8, world)
     my_rows = rows_of[rank]
-    max_rows = max(len(r) for r in rows_of)
+    assert np.array_equal(spt.shard_rows(params), my_rows)
+    max_rows = sd.max_rows(rows_of)
 
     ren = spt.Renderer(local)
     ren.reserve(len(prims), params)
@@ -127,17 +127,13 @@ def main() -> None:
     full = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
     gather_list = ([torch.empty_like(shard) for _ in range(world)] if (rank == 0 and world > 1)
                    else None)
-    row_idx = [torch.as_tensor(r, dtype=torch.long, device="cuda") for r in rows_of]
     kstats = []
 
     def step():
         ren.render_async(prims, cam, params, shard.data_ptr(), stream.cuda_stream)
         kstats.append(ren.stats())
         if world > 1:
-            dist.gather(shard, gather_list, dst=0)
-            if rank == 0:
-                for k in range(world):
-                    full.index_copy_(0, row_idx[k], gather_list[k][: len(rows_of[k])])
+            sd.gather_rows(shard, rows_of, full, gather_list)  # one RCCL gather to rank 0
         else:
             full.copy_(shard[: len(my_rows)])
 
@@ -197,7 +193,12 @@ def main() -> None:
                                       if world > 1 else "1 GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "spt::render_kernel",
+                         "traffic": traffic,
+                         "hbm_gbs": (round(traffic / (kms.mean() * 1e-3) / 1e9, 2)
+                                     if traffic else None),
+                         "hbm_frac": (round(traffic / (kms.mean() * 1e-3) / 8e12, 5)
+                                      if traffic else None),
+                         "kernel": "spt::render_kernel",
                          "kernel_ms": round(float(kms.mean()), 3),
                          "flop_per_launch": float(flop.mean()),
                          "flop_per_sample": round(float(flop.mean()) / my_samples, 1)},
