@@ -98,9 +98,16 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # SPT_DIST_BACKEND=gloo: rehearsal mode for >1 rank on a 1-GPU box (ranks share the device,
+    # the gather goes through host memory); the real path is nccl = RCCL over xGMI.
+    backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     spt = importlib.import_module("small-pathtracer_amd")
     sd = importlib.import_module("small-pathtracer_amd.distributed")
@@ -132,8 +139,12 @@ def main() -> None:
     def step():
         ren.render_async(prims, cam, params, shard.data_ptr(), stream.cuda_stream)
         kstats.append(ren.stats())
-        if world > 1:
+        if world > 1 and backend == "nccl":
             sd.gather_rows(shard, rows_of, full, gather_list)  # one RCCL gather to rank 0
+        elif world > 1:
+            host = sd.gather_rows(shard.cpu(), rows_of, full.cpu() if rank == 0 else None)
+            if rank == 0:
+                full.copy_(host)
         else:
             full.copy_(shard[: len(my_rows)])
 
@@ -151,7 +162,8 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
