@@ -32,7 +32,8 @@ namespace spt {
 constexpr int kMaxPrims = 64;
 constexpr int kBlock = 256;
 constexpr uint32_t kGrab = 64;  // units fetched per queue atomic
-constexpr int kStatWords = 32;   // [0,8) path stats, [8,28) region stats (diagnostic build)
+constexpr int kStatWords = 32;
+constexpr bool kDefaultLdsGeo = false;   // [0,8) path stats, [8,28) region stats (diagnostic build)
 
 // 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
 // axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
@@ -101,13 +102,17 @@ __device__ __forceinline__ uint32_t tkey(float t) { return __float_as_uint(t) - 
 
 // Scene topology the kernel is specialised for: rect counts per kind (-1 = runtime loop), whether
 // spheres exist (runtime loop), and the light's grouped position (-1 = runtime).
-template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_>
+// LDSGEO: read the rect records from an LDS copy (broadcast ds_read: VGPR operands, no SALU)
+// instead of scalar loads from the constant address space.
+template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool LDSGEO_ = false>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
-  static constexpr bool SPH = SPH_;
+  static constexpr bool SPH = SPH_, LDSGEO = LDSGEO_;
 };
 using TopoCornell = Topo<6, 5, 6, false, 8>;     // rect[] of :287-311 (light = XZ #3 -> pos 8)
+using TopoCornellLds = Topo<6, 5, 6, false, 8, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
+#define SPT_LDS __attribute__((address_space(3)))
 
 struct Ray6 { float oa, ia, db, ob, dc, oc; };
 template <int AXIS>  // plane axis: 2 = z (XY rects), 1 = y (XZ), 0 = x (YZ)
@@ -118,17 +123,18 @@ __device__ __forceinline__ Ray6 ray6(f3 o, f3 d, float ix, float iy, float iz) {
 }
 
 struct RectHit { float tt; bool inb; };
-__device__ __forceinline__ RectHit rect_eval(const SPT_CONST GeoRect* g, const Ray6& r) {
+template <class GP>
+__device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   const float tt = (g->k - r.oa) * r.ia;
   const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
   const bool ia = fabsf(a - g->ma) <= g->ha, ib = fabsf(b - g->mb) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib)};
 }
 
-template <int N, int AXIS>  // nearest-hit over one kind group
-__device__ __forceinline__ void rect_group(const SPT_CONST GeoRect* g, int n_rt, int pos0,
-                                           const Ray6& r, uint32_t& tmin_key, int& pos) {
-  auto one = [&](const SPT_CONST GeoRect* gj, int q) {
+template <int N, int AXIS, class GP>  // nearest-hit over one kind group
+__device__ __forceinline__ void rect_group(GP g, int n_rt, int pos0, const Ray6& r,
+                                           uint32_t& tmin_key, int& pos) {
+  auto one = [&](GP gj, int q) {
     const RectHit h = rect_eval(gj, r);
     const uint32_t kk = tkey(h.tt);
     const bool acc = h.inb & (kk < tmin_key);
@@ -158,17 +164,18 @@ __device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d)
 template <class TP>
 __device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; }
 
-template <class TP>
-__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, const int* pos2idx,
-                                                f3 o, f3 d, float& t_out, int& id) {
+template <class TP, class GP>
+__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect,
+                                                const int* pos2idx, f3 o, f3 d, float& t_out,
+                                                int& id) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
   uint32_t tmin_key = tkey(1e20f);
   int pos = -1;
   const int nxy = n_of<TP>(TP::NXY, G->n_xy), nxz = n_of<TP>(TP::NXZ, G->n_xz);
   const int nyz = n_of<TP>(TP::NYZ, G->n_yz);
-  rect_group<TP::NXY, 2>(G->rect, nxy, 0, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
-  rect_group<TP::NXZ, 1>(G->rect + nxy, nxz, nxy, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
-  rect_group<TP::NYZ, 0>(G->rect + nxy + nxz, nyz, nxy + nxz, ray6<0>(o, d, ix, iy, iz), tmin_key,
+  rect_group<TP::NXY, 2>(rect, nxy, 0, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
+  rect_group<TP::NXZ, 1>(rect + nxy, nxz, nxy, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
+  rect_group<TP::NYZ, 0>(rect + nxy + nxz, nyz, nxy + nxz, ray6<0>(o, d, ix, iy, iz), tmin_key,
                          pos);
   if constexpr (TP::SPH) {
     const int nsph = G->n_sph, base = nxy + nxz + nyz;
@@ -187,9 +194,9 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, con
 
 // Occluders of one rect group: prims at grouped positions q accepted with t < tL (q > L) or
 // t <= tL (q < L); the light itself (q == L) is skipped.
-template <int N, int AXIS, int LPOS>
-__device__ __forceinline__ bool occl_group(const SPT_CONST GeoRect* g, int n_rt, int pos0, int L,
-                                           const Ray6& r, uint32_t after, bool occ) {
+template <int N, int AXIS, int LPOS, class GP>
+__device__ __forceinline__ bool occl_group(GP g, int n_rt, int pos0, int L, const Ray6& r,
+                                           uint32_t after, bool occ) {
   if constexpr (N >= 0 && LPOS >= 0) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -214,10 +221,10 @@ __device__ __forceinline__ bool occl_group(const SPT_CONST GeoRect* g, int n_rt,
 // NEE shadow test for a black light: identical outcome to intersect_scene() followed by
 // `id == light` (:466-467) — the light at grouped position L wins iff it is accepted at t_L, no
 // primitive before it in grouped order is accepted with t <= t_L and none after it with t < t_L.
-template <class TP>
+template <class TP, class GP>
 __device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
-                                                  const SPT_CONST SceneGeo* G, f3 o, f3 d,
-                                                  float& tL) {
+                                                  const SPT_CONST SceneGeo* G, GP rect, f3 o,
+                                                  f3 d, float& tL) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
   const int nxy = n_of<TP>(TP::NXY, G->n_xy), nxz = n_of<TP>(TP::NXZ, G->n_xz);
   const int nyz = n_of<TP>(TP::NYZ, G->n_yz);
@@ -233,17 +240,17 @@ __device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
     if (lk == SPT_RECT_XY) r = ray6<2>(o, d, ix, iy, iz);
     else if (lk == SPT_RECT_XZ) r = ray6<1>(o, d, ix, iy, iz);
     else r = ray6<0>(o, d, ix, iy, iz);
-    const RectHit h = rect_eval(G->rect + L, r);
+    const RectHit h = rect_eval(rect + L, r);
     tL = h.tt;
     ok = h.inb & (tkey(tL) < tkey(1e20f));
   }
   if (__ballot(ok) == 0) return false;
   const uint32_t after = tkey(tL);
   bool occ = false;
-  occ = occl_group<TP::NXY, 2, TP::LPOS>(G->rect, nxy, 0, L, ray6<2>(o, d, ix, iy, iz), after, occ);
-  occ = occl_group<TP::NXZ, 1, TP::LPOS>(G->rect + nxy, nxz, nxy, L, ray6<1>(o, d, ix, iy, iz),
+  occ = occl_group<TP::NXY, 2, TP::LPOS>(rect, nxy, 0, L, ray6<2>(o, d, ix, iy, iz), after, occ);
+  occ = occl_group<TP::NXZ, 1, TP::LPOS>(rect + nxy, nxz, nxy, L, ray6<1>(o, d, ix, iy, iz),
                                          after, occ);
-  occ = occl_group<TP::NYZ, 0, TP::LPOS>(G->rect + nxy + nxz, nyz, nxy + nxz, L,
+  occ = occl_group<TP::NYZ, 0, TP::LPOS>(rect + nxy + nxz, nyz, nxy + nxz, L,
                                          ray6<0>(o, d, ix, iy, iz), after, occ);
   if constexpr (TP::SPH) {
     const int nsph = G->n_sph;
@@ -277,6 +284,7 @@ template <class TP>
 __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
+  __shared__ GeoRect s_rect[TP::LDSGEO ? kMaxPrims : 1];
   {
     const SPT_CONST KParams* P = cptr(Pg);
     const SPT_CONST SceneGeo* G = cptr(P->geo);
@@ -284,9 +292,11 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
       s_prims[i] = P->prims[i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
+      if (TP::LDSGEO && i < nrect) s_rect[i] = G->rect[i];
     }
   }
   __syncthreads();
+  const SPT_LDS GeoRect* lds_rect = (const SPT_LDS GeoRect*)s_rect;
 
   const uint32_t lane = __lane_id();
   // ---- per-lane state
@@ -388,7 +398,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         carried = false;
       } else {
         SPT_REGION(4);  // path-ray intersect
-        hit = intersect_scene<TP>(cptr(P->geo), s_pos2idx, o, d, t, id);
+        const SPT_CONST SceneGeo* G = cptr(P->geo);
+        if constexpr (TP::LDSGEO) hit = intersect_scene<TP>(G, lds_rect, s_pos2idx, o, d, t, id);
+        else hit = intersect_scene<TP>(G, G->rect, s_pos2idx, o, d, t, id);
         ++n_path;
       }
       const DevPrim& H = s_prims[id];
@@ -473,10 +485,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           int ids = light_id;
           if (D->light_black) {
             SPT_REGION(6);  // shadow test
-            to_light = shadow_hits_light<TP>(D, cptr(D->geo), x, dl, ts);
+            const SPT_CONST SceneGeo* G = cptr(D->geo);
+            if constexpr (TP::LDSGEO) to_light = shadow_hits_light<TP>(D, G, lds_rect, x, dl, ts);
+            else to_light = shadow_hits_light<TP>(D, G, G->rect, x, dl, ts);
           } else {
             ids = id;
-            sh = intersect_scene<TP>(cptr(D->geo), s_pos2idx, x, dl, ts, ids);
+            const SPT_CONST SceneGeo* G = cptr(D->geo);
+            if constexpr (TP::LDSGEO) sh = intersect_scene<TP>(G, lds_rect, s_pos2idx, x, dl, ts, ids);
+            else sh = intersect_scene<TP>(G, G->rect, s_pos2idx, x, dl, ts, ids);
             to_light = ids == light_id;
           }
           ++n_shadow;
@@ -853,7 +869,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const bool cornell = g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
   const int grid = c->n_cu * (cornell ? c->blocks_per_cu_cornell : c->blocks_per_cu);
   SPT_HIP(hipEventRecord(c->ev0, stream));
-  if (cornell)
+  static const bool lds_geo = [] {  // SPT_GEO=lds|smem (A/B); default below
+    const char* e = std::getenv("SPT_GEO");
+    return e ? std::strcmp(e, "lds") == 0 : kDefaultLdsGeo;
+  }();
+  if (cornell && lds_geo)
+    hipLaunchKernelGGL(render_kernel<TopoCornellLds>, dim3(grid), dim3(kBlock), 0, stream,
+                       (const KParams*)c->d_kp);
+  else if (cornell)
     hipLaunchKernelGGL(render_kernel<TopoCornell>, dim3(grid), dim3(kBlock), 0, stream,
                        (const KParams*)c->d_kp);
   else
