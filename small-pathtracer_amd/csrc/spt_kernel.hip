@@ -292,7 +292,11 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
       s_prims[i] = P->prims[i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
-      if (TP::LDSGEO && i < nrect) s_rect[i] = G->rect[i];
+      if (TP::LDSGEO && i < nrect) {
+        const SPT_CONST GeoRect& R = G->rect[i];
+        s_rect[i].k = R.k; s_rect[i].ma = R.ma; s_rect[i].ha = R.ha;
+        s_rect[i].mb = R.mb; s_rect[i].hb = R.hb; s_rect[i].idx = R.idx;
+      }
     }
   }
   __syncthreads();
