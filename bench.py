@@ -56,15 +56,17 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
 
     threads = min(16, os.cpu_count() or 1)
     h, w, spp = params.height, params.width, params.spp
-    calib = np.linspace(0, h - 1, threads).astype(np.int32)  # one row per thread
-    t0 = time.perf_counter()
-    oracle.counter_render(prims, cam._c, params, rows=calib, threads=threads)
-    t_row = max(time.perf_counter() - t0, 1e-3) / len(calib)
-    n_rows = int(max(1, min(h, round(budget_s / t_row))))
-    rows = np.unique(np.linspace(0, h - 1, n_rows).round().astype(np.int32))  # cyclic spread
-    t0 = time.perf_counter()
-    img, st = oracle.counter_render(prims, cam._c, params, rows=rows, threads=threads)
-    dt = time.perf_counter() - t0
+    # Grow an evenly spread row subset until one timed run takes >= budget_s / 2 (the first,
+    # one-row-per-thread run also absorbs library load and OpenMP start-up).
+    n_rows = threads
+    while True:
+        rows = np.unique(np.linspace(0, h - 1, n_rows).round().astype(np.int32))
+        t0 = time.perf_counter()
+        img, st = oracle.counter_render(prims, cam._c, params, rows=rows, threads=threads)
+        dt = time.perf_counter() - t0
+        if dt >= budget_s / 2 or len(rows) >= h:
+            break
+        n_rows = int(min(h, max(2 * n_rows, round(n_rows * budget_s / max(dt, 1e-3)))))
     samples = len(rows) * w * spp
     exact = gpu_img is not None and np.array_equal(gpu_img[rows], img)
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
@@ -84,7 +86,7 @@ def main() -> None:
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
     ap.add_argument("--spp", type=int, default=0, help="override spp (per-GPU for weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
                     help="PMC traffic summary (HBM bytes per render launch) to attach, if present")
     ap.add_argument("--save-ppm", default="")
