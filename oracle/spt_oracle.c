@@ -514,11 +514,23 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb) {
   spt_oracle_sincos2pi(xi1, &s, &c);
   r2s = xi2 * spt_oracle_rsq_nr(xi2);
   s1 = (1.0f - xi2) * spt_oracle_rsq_nr(1.0f - xi2);
+  cr = c * r2s;
+  sr = s * r2s;
+  if ((nl.y == 0.0f && nl.z == 0.0f && fabsf(nl.x) == 1.0f) ||
+      (nl.x == 0.0f && nl.z == 0.0f && fabsf(nl.y) == 1.0f) ||
+      (nl.x == 0.0f && nl.y == 0.0f && fabsf(nl.z) == 1.0f)) {
+    /* Contract: an axis-aligned normal (every rectangle's, smallpt.cpp:123,:166,:209) makes the
+       frame of :345-346 a signed permutation of the axes, so the direction is written out:
+       nl = (sx,0,0) -> (sx*s1, sr, -sx*cr); (0,sy,0) -> (sr, sy*s1, sy*cr);
+       (0,0,sz) -> (sr, -sz*cr, sz*s1). Same values as the general formula below up to the sign
+       of exact zeros. */
+    if (nl.x != 0.0f) return fnormalize(fv3(nl.x * s1, sr, -(nl.x * cr)));
+    if (nl.y != 0.0f) return fnormalize(fv3(sr, nl.y * s1, nl.y * cr));
+    return fnormalize(fv3(sr, -(nl.z * cr), nl.z * s1));
+  }
   a = fabsf(nl.x) > 0.1f ? fv3(nl.z, 0.0f, -nl.x) : fv3(0.0f, -nl.z, nl.y);
   u = fnormalize(a);
   v = fcross(nl, u);
-  cr = c * r2s;
-  sr = s * r2s;
   return fnormalize(fv3(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)),
                         fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
                         fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr))));

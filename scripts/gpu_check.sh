@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 rocm-smi --showproductname > gpurun_out/gpu_info.txt 2>&1 || true
+timeout -k 10 90 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke0.log 2>&1 || { echo "pre-smoke failed $?"; cat gpurun_out/smoke0.log | tail -5; exit 3; }
 timeout -k 10 420 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest -m gpu exit $rc"; tail -5 gpurun_out/pytest_gpu.log

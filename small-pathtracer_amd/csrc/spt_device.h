@@ -107,21 +107,36 @@ __device__ __forceinline__ void sincos2pi(float xi, float& s_out, float& c_out) 
   c_out = (k == 1 || k == 2) ? -ca : ca;
 }
 
-// random_scattering :337-347 (cosine-weighted hemisphere about nl).
-__device__ __forceinline__ f3 cosine_dir(f3 nl, uint32_t ra, uint32_t rb) {
+// random_scattering :337-347 (cosine-weighted hemisphere about nl), before the final normalize
+// (the kernel shares that normalize with the camera ray, :536). AXIS: nl is known to be
+// axis-aligned (rect-only scenes); otherwise it is tested per lane, as the oracle does.
+template <bool AXIS = false>
+__device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb) {
   const float xi1 = u01(ra), xi2 = u01(rb);
   float s, c;
   sincos2pi(xi1, s, c);
   const float r2s = xi2 * rsq_nr(xi2);  // sqrt(r2); xi2 = 0 gives 0
   const float om = 1.0f - xi2;
   const float s1 = om * rsq_nr(om);     // sqrt(1 - r2)
+  const float cr = c * r2s, sr = s * r2s;
+  // Contract: an axis-aligned normal (every rectangle's, :123,:166,:209) makes the frame of
+  // :345-346 a signed permutation of the axes: (sx,0,0) -> (sx*s1, sr, -sx*cr);
+  // (0,sy,0) -> (sr, sy*s1, sy*cr); (0,0,sz) -> (sr, -sz*cr, sz*s1) (oracle c_cosine).
+  const bool ax = nl.x != 0.0f, ay = nl.y != 0.0f;
+  if (AXIS || (fabsf(nl.x) + fabsf(nl.y) + fabsf(nl.z) == 1.0f &&
+               ((int)(nl.x == 0.0f) + (int)(nl.y == 0.0f) + (int)(nl.z == 0.0f)) == 2)) {
+    const float sg = ax ? nl.x : (ay ? nl.y : nl.z);
+    const float p = sg * s1, q = sg * cr;
+    return mk(ax ? p : sr, ax ? sr : (ay ? p : -q), ax ? -q : (ay ? q : p));
+  }
   const f3 a = fabsf(nl.x) > 0.1f ? mk(nl.z, 0.0f, -nl.x) : mk(0.0f, -nl.z, nl.y);
   const f3 u = normalize3(a);
   const f3 v = cross3(nl, u);
-  const float cr = c * r2s, sr = s * r2s;
-  return normalize3(mk(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)),
-                       fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
-                       fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr))));
+  return mk(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)), fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
+            fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr)));
+}
+__device__ __forceinline__ f3 cosine_dir(f3 nl, uint32_t ra, uint32_t rb) {
+  return normalize3(cosine_vec(nl, ra, rb));
 }
 
 // 1.31 fixed-point per-sample contribution (order-independent, exact integer accumulation):

@@ -26,14 +26,22 @@
 #include "../../include/spt.h"
 #include "../../include/spt_flops.h"
 #include "spt_device.h"
+#include "spt_cornell.h"
 
 namespace spt {
+
+// Rect-test formulation (A/B): 0 = SALU mask logic, 1/2 = lane-mask selects (see rect_group).
+#ifndef SPT_RECT_FORM
+#define SPT_RECT_FORM 0
+#endif
 
 constexpr int kMaxPrims = 64;
 constexpr int kBlock = 256;
 constexpr uint32_t kGrab = 64;  // units fetched per queue atomic
 constexpr int kStatWords = 32;
-constexpr bool kDefaultLdsGeo = false;   // [0,8) path stats, [8,28) region stats (diagnostic build)
+// Exit condition every wave reaches even if a path never terminated: a C3 wave runs ~4e3
+// iterations and a 1-GPU C5 wave ~3e6; stats[0] counts waves that hit the cap.
+constexpr uint32_t kMaxWaveIters = 1u << 26;  // [0,8) path stats, [8,28) region stats (diagnostic build)
 
 // 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
 // axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
@@ -100,19 +108,29 @@ __device__ __forceinline__ const SPT_CONST T* cptr(const T* p) {
 // index through LDS once per ray.
 __device__ __forceinline__ uint32_t tkey(float t) { return __float_as_uint(t) - 1u; }
 
+// Rect geometry with literal operands: kCornellRects[i] at a compile-time i (spt_cornell.h).
+struct CornellRectPtr {
+  int i;
+  __device__ constexpr CornellRectPtr operator+(int j) const { return CornellRectPtr{i + j}; }
+  __device__ constexpr const CRect* operator->() const { return &kCornellRects[i]; }
+};
+
 // Scene topology the kernel is specialised for: rect counts per kind (-1 = runtime loop), whether
-// spheres exist (runtime loop), and the light's grouped position (-1 = runtime).
-// LDSGEO: read the rect records from an LDS copy (broadcast ds_read: VGPR operands, no SALU)
-// instead of scalar loads from the constant address space.
-template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool LDSGEO_ = false>
+// spheres exist (runtime loop), the light's grouped position (-1 = runtime), and whether the rect
+// bounds are the compile-time HEAD scene (CONSTGEO) or read from the uploaded scene (s_load).
+template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
-  static constexpr bool SPH = SPH_, LDSGEO = LDSGEO_;
+  static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_;
 };
 using TopoCornell = Topo<6, 5, 6, false, 8>;     // rect[] of :287-311 (light = XZ #3 -> pos 8)
-using TopoCornellLds = Topo<6, 5, 6, false, 8, true>;
+using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
-#define SPT_LDS __attribute__((address_space(3)))
+template <class TP>
+__device__ __forceinline__ auto rects_of(const SPT_CONST SceneGeo* G) {
+  if constexpr (TP::CONSTGEO) return CornellRectPtr{0};
+  else return G->rect + 0;
+}
 
 struct Ray6 { float oa, ia, db, ob, dc, oc; };
 template <int AXIS>  // plane axis: 2 = z (XY rects), 1 = y (XZ), 0 = x (YZ)
@@ -135,11 +153,27 @@ template <int N, int AXIS, class GP>  // nearest-hit over one kind group
 __device__ __forceinline__ void rect_group(GP g, int n_rt, int pos0, const Ray6& r,
                                            uint32_t& tmin_key, int& pos) {
   auto one = [&](GP gj, int q) {
+#if SPT_RECT_FORM == 0
     const RectHit h = rect_eval(gj, r);
     const uint32_t kk = tkey(h.tt);
     const bool acc = h.inb & (kk < tmin_key);
     tmin_key = acc ? kk : tmin_key;
     pos = acc ? q : pos;
+#else
+    // bounds folded into the key with lane-mask selects (no SALU mask logic, short chain)
+    const float tt = (gj->k - r.oa) * r.ia;
+    const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
+    const bool ia = fabsf(a - gj->ma) <= gj->ha, ib = fabsf(b - gj->mb) <= gj->hb;
+    uint32_t kk = tkey(tt);
+    kk = ia ? kk : 0xFFFFFFFFu;
+#if SPT_RECT_FORM == 1
+    asm volatile("" : "+v"(kk));
+#endif
+    kk = ib ? kk : 0xFFFFFFFFu;
+    const bool acc = kk < tmin_key;
+    tmin_key = acc ? kk : tmin_key;
+    pos = acc ? q : pos;
+#endif
   };
   if constexpr (N >= 0) {
 #pragma unroll
@@ -192,76 +226,36 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   return tmin < 1e20f;
 }
 
-// Occluders of one rect group: prims at grouped positions q accepted with t < tL (q > L) or
-// t <= tL (q < L); the light itself (q == L) is skipped.
-template <int N, int AXIS, int LPOS, class GP>
-__device__ __forceinline__ bool occl_group(GP g, int n_rt, int pos0, int L, const Ray6& r,
-                                           uint32_t after, bool occ) {
-  if constexpr (N >= 0 && LPOS >= 0) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const int q = pos0 + j;  // compile-time when pos0 is
-      if (q == LPOS) continue;
-      const RectHit h = rect_eval(g + j, r);
-      const uint32_t kk = tkey(h.tt);
-      occ |= h.inb & (q < LPOS ? kk <= after : kk < after);
-    }
-  } else {
-    for (int j = 0; j < n_rt; ++j) {
-      const int q = pos0 + j;
-      if (q == L) continue;
-      const RectHit h = rect_eval(g + j, r);
-      const uint32_t kk = tkey(h.tt);
-      occ |= h.inb & ((kk < after) | ((kk == after) & (q < L)));
-    }
-  }
-  return occ;
-}
-
-// NEE shadow test for a black light: identical outcome to intersect_scene() followed by
-// `id == light` (:466-467) — the light at grouped position L wins iff it is accepted at t_L, no
-// primitive before it in grouped order is accepted with t <= t_L and none after it with t < t_L.
+// NEE pre-test (light_sampling :363-369 + the shadow ray of :466): is the light itself accepted
+// on the ray (x, dl)? Only then can the nearest hit be the light (:467), so only these rays are
+// traced against the scene. Bit-identical to the light's own test inside intersect_scene().
 template <class TP, class GP>
-__device__ __forceinline__ bool shadow_hits_light(const SPT_CONST KParams* P,
-                                                  const SPT_CONST SceneGeo* G, GP rect, f3 o,
-                                                  f3 d, float& tL) {
-  const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
-  const int nxy = n_of<TP>(TP::NXY, G->n_xy), nxz = n_of<TP>(TP::NXZ, G->n_xz);
-  const int nyz = n_of<TP>(TP::NYZ, G->n_yz);
-  const int nrect = nxy + nxz + nyz;
-  const int lk = P->light_kind;
-  const int L = TP::LPOS >= 0 ? TP::LPOS : (lk == SPT_SPHERE ? nrect + P->light_pos : P->light_pos);
-  bool ok;
-  if (TP::LPOS < 0 && lk == SPT_SPHERE) {
-    tL = sphere_t(G->sph[L - nrect], o, d);
-    ok = tkey(tL) < tkey(1e20f);
-  } else {
-    Ray6 r;
-    if (lk == SPT_RECT_XY) r = ray6<2>(o, d, ix, iy, iz);
-    else if (lk == SPT_RECT_XZ) r = ray6<1>(o, d, ix, iy, iz);
-    else r = ray6<0>(o, d, ix, iy, iz);
-    const RectHit h = rect_eval(rect + L, r);
-    tL = h.tt;
-    ok = h.inb & (tkey(tL) < tkey(1e20f));
-  }
-  if (__ballot(ok) == 0) return false;
-  const uint32_t after = tkey(tL);
-  bool occ = false;
-  occ = occl_group<TP::NXY, 2, TP::LPOS>(rect, nxy, 0, L, ray6<2>(o, d, ix, iy, iz), after, occ);
-  occ = occl_group<TP::NXZ, 1, TP::LPOS>(rect + nxy, nxz, nxy, L, ray6<1>(o, d, ix, iy, iz),
-                                         after, occ);
-  occ = occl_group<TP::NYZ, 0, TP::LPOS>(rect + nxy + nxz, nyz, nxy + nxz, L,
-                                         ray6<0>(o, d, ix, iy, iz), after, occ);
-  if constexpr (TP::SPH) {
-    const int nsph = G->n_sph;
-    for (int j = 0; j < nsph; ++j) {
-      const int q = nrect + j;
-      if (q == L) continue;
-      const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
-      occ |= (kk < after) | ((kk == after) & (q < L));
+__device__ __forceinline__ bool light_accepts(const SPT_CONST KParams* P, const SPT_CONST SceneGeo* G,
+                                              GP rect, f3 o, f3 d) {
+  if constexpr (TP::LPOS >= 0) {
+    constexpr int L = TP::LPOS;  // compile-time kind from the grouped position
+    static_assert(TP::NXY >= 0 && TP::NXZ >= 0, "LPOS needs static group sizes");
+    if constexpr (L < TP::NXY) {
+      const RectHit h = rect_eval(rect + L, Ray6{o.z, rcp_nr(d.z), d.x, o.x, d.y, o.y});
+      return h.inb & (tkey(h.tt) < tkey(1e20f));
+    } else if constexpr (L < TP::NXY + TP::NXZ) {
+      const RectHit h = rect_eval(rect + L, Ray6{o.y, rcp_nr(d.y), d.x, o.x, d.z, o.z});
+      return h.inb & (tkey(h.tt) < tkey(1e20f));
+    } else {
+      const RectHit h = rect_eval(rect + L, Ray6{o.x, rcp_nr(d.x), d.y, o.y, d.z, o.z});
+      return h.inb & (tkey(h.tt) < tkey(1e20f));
     }
+  } else {
+    const int lk = P->light_kind, L = P->light_pos;
+    if (L < 0) return false;
+    if (lk == SPT_SPHERE) return tkey(sphere_t(G->sph[L], o, d)) < tkey(1e20f);
+    Ray6 r;
+    if (lk == SPT_RECT_XY) r = Ray6{o.z, rcp_nr(d.z), d.x, o.x, d.y, o.y};
+    else if (lk == SPT_RECT_XZ) r = Ray6{o.y, rcp_nr(d.y), d.x, o.x, d.z, o.z};
+    else r = Ray6{o.x, rcp_nr(d.x), d.y, o.y, d.z, o.z};
+    const RectHit h = rect_eval(rect + L, r);
+    return h.inb & (tkey(h.tt) < tkey(1e20f));
   }
-  return ok & !occ;
 }
 
 // Diagnostic build (-DSPT_REGION_STATS): per code region, wave executions and active lanes,
@@ -280,11 +274,33 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Cost probes (diagnostic builds, -DSPT_PROBE=<bitmask>): a region is computed a second time on
+// opaque copies of its inputs and the copy is selected under an always-false opaque predicate, so
+// the image and the path statistics are unchanged and the time difference is the region's
+// marginal cost. 1 Philox, 2 trace, 8 cosine, 16 camera.
+#ifndef SPT_PROBE
+#define SPT_PROBE 0
+#endif
+template <typename T>
+__device__ __forceinline__ T opq(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// One lane = one pixel-sample path at a time, and every iteration traces exactly ONE ray per lane
+// with the same nearest-hit loop (intersect :323-335): either the path ray toward the next vertex
+// or, after a NEE event whose light sample passes light_accepts(), the shadow ray of :466. The
+// wave never runs an occlusion test for lanes that have none (the light pre-test rejects ~75% of
+// the NEE samples at HEAD); a lane whose shadow ray is pending simply skips the ray-generation and
+// shading blocks of that iteration. Per lane the arithmetic is exactly the counter-mode contract
+// (oracle c_path): only the schedule differs.
+//   iteration: [retire / refill units] -> [generate: cosine continuation or camera ray, one
+//   Philox call, shared normalize] -> [trace] -> [resolve a shadow ray] -> [shade a vertex: RR,
+//   NEE pre-test] -> [path end: accumulate].
 template <class TP>
 __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
-  __shared__ GeoRect s_rect[TP::LDSGEO ? kMaxPrims : 1];
   {
     const SPT_CONST KParams* P = cptr(Pg);
     const SPT_CONST SceneGeo* G = cptr(P->geo);
@@ -292,52 +308,56 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
       s_prims[i] = P->prims[i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
-      if (TP::LDSGEO && i < nrect) {
-        const SPT_CONST GeoRect& R = G->rect[i];
-        s_rect[i].k = R.k; s_rect[i].ma = R.ma; s_rect[i].ha = R.ha;
-        s_rect[i].mb = R.mb; s_rect[i].hb = R.hb; s_rect[i].idx = R.idx;
-      }
     }
   }
   __syncthreads();
-  const SPT_LDS GeoRect* lds_rect = (const SPT_LDS GeoRect*)s_rect;
 
   const uint32_t lane = __lane_id();
   // ---- per-lane state
-  bool has_unit = false, need_cam = true, carried = false, c_hit = false;
+  bool has_unit = false;  // owns a work unit (pixel, sample range)
+  bool gen = false;       // needs a new path ray: camera (cont == false) or cosine continuation
+  bool cont = false;
+  bool shadow = false;    // the pending ray is a NEE shadow ray from vertex o
   uint32_t lp = 0, s = 0, s_end = 0, pix = 0;
-  int px = 0, py = 0, depth = 0, c_id = 0;
-  float c_t = 0.0f;
+  int px = 0, py = 0, depth = 0, vid = 0;
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
-  f3 o = mk(0, 0, 0), d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0);
+  f3 o = mk(0, 0, 0), d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
+  u4 r = u4{0, 0, 0, 0};  // Philox words of the vertex the pending path ray leads to
   // ---- wave-uniform state
   uint32_t pool_next = 0, pool_end = 0;
-  bool exhausted = false;
-  // per-lane event counters (VALU adds under the event's own exec mask; reduced once per wave)
+  bool exhausted = false, capped = false;
+  // Wave-uniform event counters (SGPRs), fed by ballots at convergent points of the loop: per-lane
+  // counters incremented inside the divergent blocks cost ~40 VGPRs of copies.
   uint32_t n_path = 0, n_shadow = 0, n_vert = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
   uint32_t reg_flags = 0;
 #endif
 
-  for (;;) {
+  for (uint32_t iter = 0;; ++iter) {
     const SPT_CONST KParams* P = cptr(Pg);
-    // 1) retire finished units: flush the fixed-point sums of their pixel.
     SPT_REGION(0);  // loop iteration
-    if (has_unit && need_cam && s >= s_end) {
-      SPT_REGION(1);  // unit retire
+    if (iter >= kMaxWaveIters) {  // runaway guard: drop the work, leave through the normal exit
+      capped = true;                // (a second loop exit would duplicate the loop state)
+      exhausted = true;
+      has_unit = false;
+    }
+    // 1) retire finished units: flush the fixed-point sums of their pixel.
+    if (has_unit && gen && !cont && s >= s_end) {
+      SPT_REGION(1);
       unsigned long long* a = P->accum + 3ull * lp;
       if (acc0) atomicAdd(a + 0, acc0);
       if (acc1) atomicAdd(a + 1, acc1);
       if (acc2) atomicAdd(a + 2, acc2);
       acc0 = acc1 = acc2 = 0;
       has_unit = false;
+      gen = false;
     }
     // 2) refill idle lanes from the wave's pool (ballot + mbcnt prefix sum), pool from the queue.
     bool needs_unit = !has_unit;
     uint64_t need = __ballot(needs_unit);
     while (need != 0 && !exhausted) {
-      SPT_REGION(2);  // refill
+      SPT_REGION(2);
       const SPT_CONST KParams* Q = cptr(Pg);
       if (pool_next >= pool_end) {
         uint32_t b = 0;
@@ -364,193 +384,209 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         pix = (uint32_t)py * w + (uint32_t)px;
         has_unit = true;
         needs_unit = false;
-        need_cam = true;
+        gen = true;
+        cont = false;
       }
       pool_next += min((uint32_t)__popcll(need), avail);
       need = __ballot(needs_unit);
     }
     if (__ballot(has_unit) == 0) break;
+    n_cos += (uint32_t)__popcll(__ballot(gen && cont));
+    // per-lane events of this iteration, counted by ballot at its end
+    bool e_vert = false, e_miss = false, e_nee = false, e_hit = false;
 
-    if (has_unit) {
-      ++n_vert;
-      // One Philox call per lane per iteration, for the vertex about to be shaded: top 24 bits of
-      // r.x..r.w = light x, light z, scatter xi1, xi2; low bytes = RR draw (r.x, r.y) and NEE-mix
-      // draw (r.z, r.w) — at vertex 1 the low bytes are the camera jitter instead.
-      const u4 r = philox4x32_10(pix, s, need_cam ? 1u : (uint32_t)depth + 1u, cptr(Pg)->seed);
-      // 3) camera ray for lanes starting a sample (:533-536).
-      if (need_cam) {
-        SPT_REGION(3);  // camera ray
+    // 3) generate the path ray: the cosine continuation from the last vertex (random_scattering
+    //    :337-347, its xi from that vertex's Philox words) or the camera ray of a new sample
+    //    (:533-536, jitter from the low bytes of vertex 1's words), one Philox call for the
+    //    vertex the ray leads to, one normalize for both.
+    if (gen) {
+      f3 v = mk(0, 0, 0);
+      if (cont) {
+        SPT_REGION(8);
+        v = cosine_vec<!TP::SPH>(nl, r.z, r.w);
+        if (SPT_PROBE & 8) {
+          const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w);
+          if (opq(0u) != 0u) v = v2;
+        }
+      }
+      r = philox4x32_10(pix, s, cont ? (uint32_t)depth + 1u : 1u, cptr(Pg)->seed);
+      if (SPT_PROBE & 1) {
+        const u4 r2 = philox4x32_10(opq(pix), s, cont ? (uint32_t)depth + 1u : 1u, cptr(Pg)->seed);
+        if (opq(0u) != 0u) r = r2;
+      }
+      if (!cont) {
+        SPT_REGION(3);
         const SPT_CONST KParams* C = cptr(Pg);
         const float su = (((float)px - 0.5f) + u16(r.x, r.y)) * C->inv_w;
         const float sv = (((float)(C->height - py - 1) - 0.5f) + u16(r.z, r.w)) * C->inv_h;
         o = mk(C->cam[0], C->cam[1], C->cam[2]);
-        d = normalize3(mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
-                          fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
-                          fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]));
+        v = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
+               fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
+               fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
         T = mk(1, 1, 1);
         L = mk(0, 0, 0);
         depth = 0;
-        carried = false;
-        need_cam = false;
       }
-      // 4) vertex: hittingPoint :371-377 (or the hit carried from a NEE shadow ray).
-      int id = 0;
+      d = normalize3(v);
+      shadow = false;
+      gen = false;
+    }
+
+    n_path += (uint32_t)__popcll(__ballot(has_unit && !shadow));
+    if (has_unit) {
+      // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
+      SPT_REGION(4);
+      const SPT_CONST SceneGeo* G = cptr(P->geo);
+      int id = shadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
       float t;
-      bool hit;
-      if (carried) {
-        hit = c_hit; t = c_t; id = hit ? c_id : 0;
-        carried = false;
-      } else {
-        SPT_REGION(4);  // path-ray intersect
-        const SPT_CONST SceneGeo* G = cptr(P->geo);
-        if constexpr (TP::LDSGEO) hit = intersect_scene<TP>(G, lds_rect, s_pos2idx, o, d, t, id);
-        else hit = intersect_scene<TP>(G, G->rect, s_pos2idx, o, d, t, id);
-        ++n_path;
+      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, o, d, t, id);
+      if (SPT_PROBE & 2) {
+        float t2;
+        int id2 = id;
+        const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2);
+        if (opq(0u) != 0u) { hit = h2; t = t2; id = id2; }
       }
-      const DevPrim& H = s_prims[id];
-      const int kind = H.kind;
-      f3 x;
-      if (!hit) {
-        x = mk(0, 0, 0);
-        ++n_miss;
-      } else {
-        float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
-        if (kind == SPT_RECT_XY) tr = (H.w1 - o.z) / d.z;
-        else if (kind == SPT_RECT_XZ) tr = (H.w1 - o.y) / d.y;
-        else if (kind == SPT_RECT_YZ) tr = (H.w1 - o.x) / d.x;
-        x = mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
-      }
-      f3 nl;  // Hitable::normal, oriented against the ray (:123,:166,:209,:251)
-      if (kind == SPT_RECT_XY) nl = d.z < 0.0f ? mk(0, 0, 1) : mk(0, 0, -1);
-      else if (kind == SPT_RECT_XZ) nl = d.y < 0.0f ? mk(0, 1, 0) : mk(0, -1, 0);
-      else if (kind == SPT_RECT_YZ) nl = d.x < 0.0f ? mk(1, 0, 0) : mk(-1, 0, 0);
-      else {
-        const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
-        nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
-      }
-      f3 f = mk(H.cx, H.cy, H.cz);
-      const f3 e = mk(H.ex, H.ey, H.ez);
-      const float p = H.pmax;
-      ++depth;
-      u4 rl = r;  // RR / NEE-mix draws; at vertex 1 from stream 1 (only configs that need them)
-      if (depth == 1) {
-        const SPT_CONST KParams* C = cptr(Pg);
-        if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
-          rl = philox4x32_10(pix, s, 1u | 0x80000000u, C->seed);
-      }
-      // Russian roulette :448-454 (+ optional hard depth cap).
-      bool term = false;
-      const int max_depth = P->max_depth;
-      if (max_depth > 0 && depth >= max_depth) {
-        term = true;
-      } else if (depth > P->rr_depth || p == 0.0f) {
-        if (!(p > 0.0f)) {
-          term = true;
+      bool vertex = !shadow, term = false;
+
+      // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467).
+      if (shadow) {
+        SPT_REGION(6);
+        const SPT_CONST KParams* D = cptr(Pg);
+        if (id == D->light_id) {
+          SPT_REGION(7);
+          e_hit = true;
+          const float pdf = fabsf((D->larea * d.y) / (t * t));           // :471
+          const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
+          const float w = pdf * brdf;
+          T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
+          // The light hit by this very ray is the next vertex, shaded in the common block below.
+          // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
+          // random draw; anything else is shaded with that vertex's own Philox words.
+          if (!(hit && s_prims[id].pmax == 0.0f))
+            r = philox4x32_10(pix, s, (uint32_t)depth + 1u, D->seed);
+          vertex = true;
         } else {
-          bool keep = true;
-          if (p < 1.0f) keep = u16(rl.x, rl.y) < p;
-          if (keep) {
-            const float ip = 1.0f / p;
-            f = mk(f.x * ip, f.y * ip, f.z * ip);
-          } else {
-            term = true;
-          }
+          gen = true;  // occluded: continue with the cosine sample (:468-469), T = T*f
+          cont = true;
         }
+        shadow = false;
       }
-      if (!term) {
-        SPT_REGION(5);  // DIFF shading (continuing vertex)
-        // DIFF :457-480.
-        const SPT_CONST KParams* C = cptr(Pg);
-        bool nee;
-        const float q = C->nee_prob;
-        if (q >= 1.0f) nee = true;
-        else if (q <= 0.0f) nee = false;
-        else nee = u16(rl.z, rl.w) < q;
-        float w = 1.0f;
-        f3 dn;
-        bool light_end = false;
-        f3 e_light = mk(0, 0, 0);
-        bool scatter = true;
-        if (nee) {
-          // light_sampling :363-369, shadow ray :466, NEE weight :471-472.
-          const SPT_CONST KParams* D = cptr(Pg);
-          float xl, zl;
-          if (D->light_mode == SPT_LIGHT_GLIBC_WRAP) {
-            xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * D->ldxi), 0x1p-31f, D->lx0);
-            zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * D->ldzi), 0x1p-31f, D->lz0);
+
+      // 6) shade a vertex (:422, :444-480).
+      if (vertex) {
+        SPT_REGION(5);
+        e_vert = true;
+        const DevPrim& H = s_prims[id];
+        const int kind = H.kind;
+        f3 x;
+        if (!hit) {
+          x = mk(0, 0, 0);
+          e_miss = true;
+        } else {
+          float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
+          if (kind == SPT_RECT_XY) tr = (H.w1 - o.z) / d.z;
+          else if (kind == SPT_RECT_XZ) tr = (H.w1 - o.y) / d.y;
+          else if (kind == SPT_RECT_YZ) tr = (H.w1 - o.x) / d.x;
+          x = mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
+        }
+        // Hitable::normal, oriented against the ray (:123,:166,:209,:251)
+        if (kind == SPT_RECT_XY) nl = d.z < 0.0f ? mk(0, 0, 1) : mk(0, 0, -1);
+        else if (kind == SPT_RECT_XZ) nl = d.y < 0.0f ? mk(0, 1, 0) : mk(0, -1, 0);
+        else if (kind == SPT_RECT_YZ) nl = d.x < 0.0f ? mk(1, 0, 0) : mk(-1, 0, 0);
+        else {
+          const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
+          nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
+        }
+        f3 f = mk(H.cx, H.cy, H.cz);
+        const f3 e = mk(H.ex, H.ey, H.ez);
+        const float p = H.pmax;
+        ++depth;
+        u4 rl = r;  // RR / NEE-mix draws; at vertex 1 from stream 1 (only configs that need them)
+        if (depth == 1) {
+          const SPT_CONST KParams* C = cptr(Pg);
+          if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
+            rl = philox4x32_10(pix, s, 1u | 0x80000000u, C->seed);
+        }
+        // Russian roulette :448-454 (+ optional hard depth cap).
+        const int max_depth = P->max_depth;
+        if (max_depth > 0 && depth >= max_depth) {
+          term = true;
+        } else if (depth > P->rr_depth || p == 0.0f) {
+          if (!(p > 0.0f)) {
+            term = true;
           } else {
-            xl = fmaf(u01(r.x), D->ldx, D->lx0);
-            zl = fmaf(u01(r.y), D->ldz, D->lz0);
-          }
-          const f3 dl = normalize3(mk(xl - x.x, D->ly - x.y, zl - x.z));
-          const int light_id = D->light_id;
-          float ts;
-          bool to_light, sh = true;
-          int ids = light_id;
-          if (D->light_black) {
-            SPT_REGION(6);  // shadow test
-            const SPT_CONST SceneGeo* G = cptr(D->geo);
-            if constexpr (TP::LDSGEO) to_light = shadow_hits_light<TP>(D, G, lds_rect, x, dl, ts);
-            else to_light = shadow_hits_light<TP>(D, G, G->rect, x, dl, ts);
-          } else {
-            ids = id;
-            const SPT_CONST SceneGeo* G = cptr(D->geo);
-            if constexpr (TP::LDSGEO) sh = intersect_scene<TP>(G, lds_rect, s_pos2idx, x, dl, ts, ids);
-            else sh = intersect_scene<TP>(G, G->rect, s_pos2idx, x, dl, ts, ids);
-            to_light = ids == light_id;
-          }
-          ++n_shadow;
-          if (to_light) {
-            SPT_REGION(7);  // NEE light hit
-            ++n_nee_hit;
-            const float pdf = fabsf((cptr(Pg)->larea * dl.y) / (ts * ts));
-            const float brdf = fabsf(dot3(dl, nl) * 0.318309886183790672f);
-            w = pdf * brdf;
-            dn = dl;
-            scatter = false;
-            if (sh && s_prims[ids].pmax == 0.0f) {
-              // The next vertex is the (black) light hit by this very ray: RR with p == 0 ends
-              // the path there (:448-453) returning its emission — finish it inline.
-              light_end = true;
-              e_light = mk(s_prims[ids].ex, s_prims[ids].ey, s_prims[ids].ez);
+            bool keep = true;
+            if (p < 1.0f) keep = u16(rl.x, rl.y) < p;
+            if (keep) {
+              const float ip = 1.0f / p;
+              f = mk(f.x * ip, f.y * ip, f.z * ip);
             } else {
-              carried = true; c_hit = sh; c_t = ts; c_id = ids;
+              term = true;
             }
           }
         }
-        if (scatter) {
-          SPT_REGION(8);  // cosine direction
-          dn = cosine_dir(nl, r.z, r.w);
-          ++n_cos;
-        }
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
-        T = mk((T.x * f.x) * w, (T.y * f.y) * w, (T.z * f.z) * w);
-        o = x;
-        d = dn;
-        if (light_end) {
-          ++n_vert;
-          L = mk(fmaf(T.x, e_light.x, L.x), fmaf(T.y, e_light.y, L.y), fmaf(T.z, e_light.z, L.z));
-          term = true;
+        if (!term) {
+          // DIFF :457-480. T becomes T*f now; the NEE weight (if the light is reached) multiplies
+          // it when the shadow ray resolves, so T = (T*f)*w exactly as the contract rounds it.
+          T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
+          o = x;
+          const SPT_CONST KParams* D = cptr(Pg);
+          const float q = D->nee_prob;
+          bool nee;
+          if (q >= 1.0f) nee = true;
+          else if (q <= 0.0f) nee = false;
+          else nee = u16(rl.z, rl.w) < q;
+          bool cand = false;
+          if (nee) {
+            // light_sampling :363-369 and the shadow-ray direction :466.
+            float xl, zl;
+            if (D->light_mode == SPT_LIGHT_GLIBC_WRAP) {
+              xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * D->ldxi), 0x1p-31f, D->lx0);
+              zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * D->ldzi), 0x1p-31f, D->lz0);
+            } else {
+              xl = fmaf(u01(r.x), D->ldx, D->lx0);
+              zl = fmaf(u01(r.y), D->ldz, D->lz0);
+            }
+            const f3 dl = normalize3(mk(xl - x.x, D->ly - x.y, zl - x.z));
+            e_nee = true;
+            const SPT_CONST SceneGeo* G2 = cptr(D->geo);
+            // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
+            cand = (id == D->light_id) || light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
+            if (cand) {
+              d = dl;
+              vid = id;
+              shadow = true;
+            }
+          }
+          if (!cand) {
+            gen = true;
+            cont = true;
+          }
         }
-      } else {
-        L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
       }
+      // 7) path end: accumulate this sample (:536-538) and start the next one.
       if (term) {
-        SPT_REGION(9);  // path end: accumulate
+        SPT_REGION(9);
         const float inv_spp = cptr(Pg)->inv_spp;
         acc0 += fix31(L.x, inv_spp);
         acc1 += fix31(L.y, inv_spp);
         acc2 += fix31(L.z, inv_spp);
         ++s;
-        need_cam = true;
+        gen = true;
+        cont = false;
       }
     }
+    n_vert += (uint32_t)__popcll(__ballot(e_vert));
+    n_miss += (uint32_t)__popcll(__ballot(e_miss));
+    n_shadow += (uint32_t)__popcll(__ballot(e_nee));
+    n_nee_hit += (uint32_t)__popcll(__ballot(e_hit));
 #ifdef SPT_REGION_STATS
 #pragma unroll
-    for (int r = 0; r < kRegions; ++r) {
-      const uint64_t m = __ballot((reg_flags >> r) & 1u);
-      reg_exec[r] += m != 0;
-      reg_lanes[r] += (uint32_t)__popcll(m);
+    for (int k = 0; k < kRegions; ++k) {
+      const uint64_t m = __ballot((reg_flags >> k) & 1u);
+      reg_exec[k] += m != 0;
+      reg_lanes[k] += (uint32_t)__popcll(m);
     }
     reg_flags = 0;
 #endif
@@ -559,22 +595,24 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     unsigned long long* st = cptr(Pg)->stats;  // wave-reduced by the atomic optimizer
 #ifdef SPT_REGION_STATS
     if (lane == 0) {  // wave-uniform values: one lane adds them
-      for (int r = 0; r < kRegions; ++r) {
-        atomicAdd(st + 8 + 2 * r, (unsigned long long)reg_exec[r]);
-        atomicAdd(st + 9 + 2 * r, (unsigned long long)reg_lanes[r]);
+      for (int k = 0; k < kRegions; ++k) {
+        atomicAdd(st + 8 + 2 * k, (unsigned long long)reg_exec[k]);
+        atomicAdd(st + 9 + 2 * k, (unsigned long long)reg_lanes[k]);
       }
     }
 #endif
-    atomicAdd(st + 1, (unsigned long long)n_path);
-    atomicAdd(st + 2, (unsigned long long)n_shadow);
-    atomicAdd(st + 3, (unsigned long long)n_vert);
-    atomicAdd(st + 4, (unsigned long long)n_shadow);
-    atomicAdd(st + 5, (unsigned long long)n_nee_hit);
-    atomicAdd(st + 6, (unsigned long long)n_cos);
-    atomicAdd(st + 7, (unsigned long long)n_miss);
+    if (lane == 0) {  // wave-uniform counters: one lane adds them
+      if (capped) atomicAdd(st + 0, 1ull);  // the host reports an error
+      atomicAdd(st + 1, (unsigned long long)n_path);
+      atomicAdd(st + 2, (unsigned long long)n_shadow);
+      atomicAdd(st + 3, (unsigned long long)n_vert);
+      atomicAdd(st + 4, (unsigned long long)n_shadow);
+      atomicAdd(st + 5, (unsigned long long)n_nee_hit);
+      atomicAdd(st + 6, (unsigned long long)n_cos);
+      atomicAdd(st + 7, (unsigned long long)n_miss);
+    }
   }
 }
-
 // 1.31 fixed point -> float, clamp :538 (values are >= 0 by construction).
 __global__ void __launch_bounds__(kBlock)
 finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict__ rgb, uint32_t n) {
@@ -609,6 +647,7 @@ struct spt_context {
   int device = 0;
   int n_cu = 0, blocks_per_cu = 0;      // generic kernel
   int blocks_per_cu_cornell = 0;        // TopoCornell specialisation
+  int blocks_per_cu_const = 0;          // TopoCornellConst (compile-time HEAD geometry)
   DevPrim* prims = nullptr;
   SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
@@ -716,6 +755,20 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
 
 static int tile_rows_of(const spt_params* p) { return p->tile_rows > 0 ? p->tile_rows : 8; }
 
+// Does the uploaded scene's grouped geometry equal the compile-time HEAD scene bit for bit?
+static bool cornell_const_match(const SceneGeo& g, int light_pos) {
+  if (g.n_xy != kCornellNXY || g.n_xz != kCornellNXZ || g.n_yz != kCornellNYZ || g.n_sph != 0 ||
+      light_pos != kCornellLightPos)
+    return false;
+  for (int i = 0; i < kCornellNXY + kCornellNXZ + kCornellNYZ; ++i) {
+    const GeoRect& R = g.rect[i];
+    const CRect& C = kCornellRects[i];
+    const float a[5] = {R.k, R.ma, R.ha, R.mb, R.hb}, b[5] = {C.k, C.ma, C.ha, C.mb, C.hb};
+    if (std::memcmp(a, b, sizeof a) != 0 || R.idx != C.idx) return false;
+  }
+  return true;
+}
+
 extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   if (!out) return fail(SPT_ERR_INVALID_ARG, "null out");
   int count = 0;
@@ -740,6 +793,11 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
           hipSuccess || bpc <= 0)
     bpc = 4;
   c->blocks_per_cu_cornell = bpc;
+  bpc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel<TopoCornellConst>, kBlock,
+                                                   0) != hipSuccess || bpc <= 0)
+    bpc = 4;
+  c->blocks_per_cu_const = bpc;
   hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
   if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
@@ -871,14 +929,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // position 8) runs a fully unrolled intersect; anything else the generic loops.
   const SceneGeo& g = *c->h_geo;
   const bool cornell = g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
-  const int grid = c->n_cu * (cornell ? c->blocks_per_cu_cornell : c->blocks_per_cu);
+  static const bool no_const = std::getenv("SPT_NO_CONST_SCENE") != nullptr;  // A/B switch
+  const bool cconst = !no_const && cornell_const_match(g, light_pos);
+  const int grid = c->n_cu * (cconst    ? c->blocks_per_cu_const
+                              : cornell ? c->blocks_per_cu_cornell
+                                        : c->blocks_per_cu);
   SPT_HIP(hipEventRecord(c->ev0, stream));
-  static const bool lds_geo = [] {  // SPT_GEO=lds|smem (A/B); default below
-    const char* e = std::getenv("SPT_GEO");
-    return e ? std::strcmp(e, "lds") == 0 : kDefaultLdsGeo;
-  }();
-  if (cornell && lds_geo)
-    hipLaunchKernelGGL(render_kernel<TopoCornellLds>, dim3(grid), dim3(kBlock), 0, stream,
+  if (cconst)
+    hipLaunchKernelGGL(render_kernel<TopoCornellConst>, dim3(grid), dim3(kBlock), 0, stream,
                        (const KParams*)c->d_kp);
   else if (cornell)
     hipLaunchKernelGGL(render_kernel<TopoCornell>, dim3(grid), dim3(kBlock), 0, stream,
@@ -913,6 +971,11 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
     std::fprintf(stderr, "\n");
   }
 #endif
+  if (h[0] != 0) {
+    c->pending = false;
+    return fail(SPT_ERR_HIP, "render kernel hit its iteration cap in " + std::to_string(h[0]) +
+                                 " waves (a path did not terminate); the image is incomplete");
+  }
   float ms = 0.0f;
   SPT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   std::memset(out, 0, sizeof *out);
