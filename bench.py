@@ -85,6 +85,7 @@ def main() -> None:
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
     ap.add_argument("--spp", type=int, default=0, help="override spp (per-GPU for weak scaling)")
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
@@ -123,7 +124,7 @@ def main() -> None:
     cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
     params = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
                                 max_depth=cfg["max_depth"], tile_rows=8, shard_index=rank,
-                                shard_count=world, device=local)
+                                shard_count=world, device=local, chunk=args.chunk)
     rows_of = sd.shard_row_lists(h, 8, world)
     my_rows = rows_of[rank]
     assert np.array_equal(spt.shard_rows(params), my_rows)

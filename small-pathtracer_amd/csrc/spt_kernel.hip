@@ -888,12 +888,13 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.tile_rows = tile_rows_of(p); K.shard_index = p->shard_index; K.shard_count = p->shard_count;
   const int rows = spt_shard_row_count(p);
   K.n_local_pix = rows * p->width;
-  // Unit size: enough units for >= 8 per resident lane so the queue drains evenly; never
-  // changes results (integer accumulation).
+  // Unit size: ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured
+  // 25.0 ms vs 26.0 ms at 8 units/lane and 27.8 ms at 2); never changes results (integer
+  // accumulation).
   int chunk = p->chunk;
   if (chunk <= 0) {
     const double lanes = (double)c->n_cu * c->blocks_per_cu * kBlock;
-    const double want_units = 8.0 * lanes;
+    const double want_units = 16.0 * lanes;
     const double per_pix = std::max(1.0, want_units / std::max(1, K.n_local_pix));
     chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
     chunk = std::min(chunk, p->spp);
