@@ -77,6 +77,58 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
             "gpu_rows_bit_exact": bool(exact)}
 
 
+def image_writer(spt, full, w, h, with_cpu: bool):
+    """§8(f) output formats: the GPU encoder (spt_image.hip) on the resident framebuffer, P3 as the
+    reference writes it (:548-551) and P6/PFM; HBM bytes = 12 B/pixel read + encoded bytes written
+    (P3 also re-reads the framebuffer in its write pass). CPU leg: the oracle's fprintf-format
+    restatement of the same writer on the same image (single thread)."""
+    import torch
+    from oracle import oracle
+
+    enc = spt.Encoder(torch.cuda.current_device())
+    out = {}
+    try:
+        for name in ("p3", "p6", "pfm"):
+            cap = spt.Encoder.bound(w, h, name)
+            buf = torch.empty(cap, dtype=torch.uint8, device="cuda")
+            stream = torch.cuda.current_stream().cuda_stream
+            n = enc.encode(full.data_ptr(), w, h, name, buf.data_ptr(), cap, stream)  # warm-up
+            torch.cuda.synchronize()
+            reps = 10
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                n = enc.encode(full.data_ptr(), w, h, name, buf.data_ptr(), cap, stream)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / reps
+            moved = w * h * 12 * (2 if name == "p3" else 1) + n
+            out[name] = {"bytes": n, "ms": round(dt * 1e3, 4), "GBps": round(moved / dt / 1e9, 1)}
+        # the C4/C5 image size (4096^2, 201 MB of fp32) with synthetic data, P3
+        big = torch.rand((4096, 4096, 3), dtype=torch.float32, device="cuda")
+        cap = spt.Encoder.bound(4096, 4096, "p3")
+        buf = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        enc.encode(big.data_ptr(), 4096, 4096, "p3", buf.data_ptr(), cap, stream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            n = enc.encode(big.data_ptr(), 4096, 4096, "p3", buf.data_ptr(), cap, stream)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / 5
+        out["p3_4096x4096_synthetic"] = {"bytes": n, "ms": round(dt * 1e3, 3),
+                                          "GBps": round((4096 * 4096 * 24 + n) / dt / 1e9, 1)}
+        del big, buf
+        if with_cpu:
+            img = full.cpu().numpy()
+            t0 = time.perf_counter()
+            b = oracle.encode_image(img, 0)
+            out["p3"]["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+            out["p3"]["cpu_kind"] = "oracle snprintf restatement of :548-551, 1 thread"
+            out["p3"]["bytes_equal_cpu"] = bool(len(b) == out["p3"]["bytes"])
+    finally:
+        enc.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -193,6 +245,7 @@ def main() -> None:
             cpu = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
         if args.save_ppm:
             spt.write_ppm(args.save_ppm, img)
+        writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -221,6 +274,7 @@ def main() -> None:
                       "rays_per_sample": round((s0["path_rays"] + s0["shadow_rays"]) / my_samples, 4),
                       "misses_per_sample": round(s0["misses"] / my_samples, 4)},
             "cpu_baseline": cpu,
+            "image_writer": writer,
         }
         print(json.dumps(out), flush=True)
     ren.close()

@@ -145,6 +145,26 @@ spt_status spt_render_async(spt_context* ctx, const spt_prim* prims, int32_t n_p
 /* Synchronises the context's last render and returns its stats. */
 spt_status spt_context_stats(spt_context* ctx, spt_stats* out);
 
+/* ---- image output (:313-321 toInt/clamp, :548-551 the P3 writer) ----
+ * The encoder turns a DEVICE framebuffer (h*w*3 floats, row-major, y=0 top: what spt_render_async
+ * writes) into file bytes on the GPU. P3 is byte-identical to the reference's fprintf loop
+ * ("P3\n%d %d\n%d\n" then "%d %d %d " per pixel, toInt = int(pow(clamp(x), 1/2.2)*255 + .5) in
+ * double); P6 is its binary form; PFM is the linear framebuffer ("PF", scale -1 = little endian,
+ * scanlines bottom to top, header padded so the floats are dword-aligned). */
+typedef enum spt_image_format { SPT_IMAGE_P3 = 0, SPT_IMAGE_P6 = 1, SPT_IMAGE_PFM = 2 } spt_image_format;
+typedef struct spt_encoder spt_encoder;
+uint64_t spt_image_bound(int32_t w, int32_t h, int32_t format); /* max encoded bytes (0 if invalid) */
+spt_status spt_encoder_create(int32_t device, spt_encoder** out);
+spt_status spt_encoder_destroy(spt_encoder* enc);
+/* Encode on `stream` into out_dev (cap bytes). *len_out = encoded length. P3's length depends on
+ * the data, so P3 synchronises `stream` once (after the length pass); P6/PFM do not. */
+spt_status spt_encode_image(spt_encoder* enc, const float* rgb_dev, int32_t w, int32_t h,
+                            int32_t format, uint8_t* out_dev, uint64_t cap, uint64_t* len_out,
+                            void* stream);
+/* Encode (rgb: host or device pointer) and write the file. Replaces the writer of :548-551. */
+spt_status spt_write_image(int32_t device, const float* rgb, int32_t w, int32_t h, int32_t format,
+                           const char* path);
+
 /* ---- introspection ---- */
 int32_t spt_abi_version(void);
 const char* spt_status_string(spt_status s);

@@ -112,6 +112,21 @@ def write_ppm(path: str, rgb: np.ndarray) -> None:
         lib().spt_oracle_write_ppm_f(path.encode(), w, h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
 
 
+def encode_image(rgb: np.ndarray, fmt: int) -> bytes:
+    """P3 (0) / P6 (1) / PFM (2) file bytes from the C restatement of :548-551 (the checker)."""
+    h, w, _ = rgb.shape
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    L = lib()
+    L.spt_oracle_encode_image.restype = ctypes.c_size_t
+    L.spt_oracle_encode_image.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    ptr = a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    need = L.spt_oracle_encode_image(ptr, w, h, fmt, None, 0)
+    buf = ctypes.create_string_buffer(need)
+    n = L.spt_oracle_encode_image(ptr, w, h, fmt, buf, need)
+    return buf.raw[:n]
+
+
 def erand48_seq(xi2: int, n: int):
     xs = (ctypes.c_ushort * 3)(0, 0, xi2 & 0xFFFF)
     return [lib().spt_oracle_erand48(xs) for _ in range(n)]

@@ -314,6 +314,53 @@ int spt_oracle_write_ppm_f(const char* path, int w, int h, const float* c) {
   return 0;
 }
 
+/* The same files in memory (test checker for the GPU encoder, spt_image.hip): format 0 = P3 exactly
+   as :549-551, 1 = P6 (bytes of toInt), 2 = PFM (little-endian floats, bottom-to-top scanlines,
+   scale text "-1.0" padded with zeros so the data starts dword-aligned). Returns the length, or
+   the needed length if cap is too small (nothing written then). */
+size_t spt_oracle_encode_image(const float* c, int w, int h, int format, unsigned char* out,
+                               size_t cap) {
+  char hd[96];
+  size_t n = 0, i;
+  const size_t np = (size_t)w * (size_t)h;
+  if (format == 0) {
+    size_t need = (size_t)snprintf(hd, sizeof hd, "P3\n%d %d\n%d\n", w, h, 255);
+    char buf[48];
+    for (i = 0; i < np; i++)
+      need += (size_t)snprintf(buf, sizeof buf, "%d %d %d ", o_toInt(c[3 * i]), o_toInt(c[3 * i + 1]),
+                               o_toInt(c[3 * i + 2]));
+    if (need > cap) return need;
+    n = (size_t)snprintf(hd, sizeof hd, "P3\n%d %d\n%d\n", w, h, 255);
+    memcpy(out, hd, n);
+    for (i = 0; i < np; i++) {
+      const int k = snprintf(buf, sizeof buf, "%d %d %d ", o_toInt(c[3 * i]), o_toInt(c[3 * i + 1]),
+                             o_toInt(c[3 * i + 2]));
+      memcpy(out + n, buf, (size_t)k);
+      n += (size_t)k;
+    }
+    return n;
+  }
+  if (format == 1) {
+    n = (size_t)snprintf(hd, sizeof hd, "P6\n%d %d\n255\n", w, h);
+    if (n + 3 * np > cap) return n + 3 * np;
+    memcpy(out, hd, n);
+    for (i = 0; i < 3 * np; i++) out[n + i] = (unsigned char)o_toInt(c[i]);
+    return n + 3 * np;
+  }
+  {
+    int y;
+    n = (size_t)snprintf(hd, sizeof hd, "PF\n%d %d\n-1.0", w, h);
+    while ((n + 1) % 4) hd[n++] = '0';
+    hd[n++] = '\n';
+    if (n + 12 * np > cap) return n + 12 * np;
+    memcpy(out, hd, n);
+    for (y = 0; y < h; y++)
+      memcpy(out + n + (size_t)(h - 1 - y) * (size_t)w * 12, c + (size_t)y * (size_t)w * 3,
+             (size_t)w * 12);
+    return n + 12 * np;
+  }
+}
+
 /* Exposed for known-answer tests. */
 double spt_oracle_erand48(unsigned short xs[3]) { return o_erand48(xs); }
 void spt_oracle_glibc_rand(unsigned seed, int n, int32_t* out) {

@@ -10,13 +10,13 @@ reference (/root/reference/src/...)    here
 ``Refl_t {DIFF, SPEC, REFR}`` :72-74    ``DIFF, SPEC, REFR``
 ``Camera`` :256-285                     ``Camera`` (constructor semantics via spt_camera_init)
 ``Hitable *rect[]`` :287-311            ``cornell_scene()``
-``clamp``/``toInt`` :314-321            ``clamp``/``toInt``
 pixel loop :528-542 (+ radiance :419)   ``render()`` / ``Renderer`` (HIP kernel, gfx950)
-PPM writer :548-551                     ``write_ppm()`` (byte-identical P3)
+``toInt`` :319-321 + PPM writer :548-551  ``write_ppm()`` / ``write_image()`` / ``Encoder``
+                                        (GPU encoder: byte-identical P3, plus P6 and PFM)
 =====================================  ==================================================
 
-The product path is the HIP kernel only: ``render()`` raises if libspt.so or a gfx950 device is
-missing — there is no CPU fallback in this package.
+The product path is the HIP kernel only: ``render()`` and the writers raise if libspt.so or a
+gfx950 device is missing — there is no CPU fallback in this package.
 """
 from __future__ import annotations
 
@@ -91,7 +91,9 @@ STAT_KEYS = ["samples", "path_rays", "shadow_rays", "vertices", "nee_events", "n
 EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_scene_spheres32",
            "spt_shard_rows", "spt_render", "spt_context_create", "spt_context_destroy",
            "spt_context_reserve", "spt_render_async", "spt_context_stats", "spt_abi_version",
-           "spt_status_string", "spt_last_error", "spt_device_count"]
+           "spt_status_string", "spt_last_error", "spt_device_count", "spt_image_bound",
+           "spt_encoder_create", "spt_encoder_destroy", "spt_encode_image", "spt_write_image"]
+IMAGE_FORMATS = {"p3": 0, "p6": 1, "pfm": 2}
 
 _lib = None
 
@@ -103,6 +105,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise SptError(2, f"{path} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1
+    # (same SONAMEs as /opt/rocm's). Loading torch first makes libspt bind to torch's copy, so
+    # device pointers and streams from torch are valid here; loading libspt first would pin the
+    # system runtime and torch's later HIP init fails ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P, I32, U32 = ctypes.POINTER, ctypes.c_int32, ctypes.c_uint32
     lib.spt_default_params.argtypes = [P(spt_params)]
@@ -125,6 +135,17 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.spt_status_string.restype = ctypes.c_char_p
     lib.spt_last_error.restype = ctypes.c_char_p
     lib.spt_device_count.restype = I32
+    U64 = ctypes.c_uint64
+    lib.spt_image_bound.argtypes = [I32, I32, I32]
+    lib.spt_image_bound.restype = U64
+    lib.spt_encoder_create.argtypes = [I32, P(ctypes.c_void_p)]
+    lib.spt_encoder_destroy.argtypes = [ctypes.c_void_p]
+    lib.spt_encode_image.argtypes = [ctypes.c_void_p, ctypes.c_void_p, I32, I32, I32,
+                                     ctypes.c_void_p, U64, P(U64), ctypes.c_void_p]
+    lib.spt_write_image.argtypes = [I32, ctypes.c_void_p, I32, I32, I32, ctypes.c_char_p]
+    for name in ("spt_encoder_create", "spt_encoder_destroy", "spt_encode_image",
+                 "spt_write_image"):
+        getattr(lib, name).restype = I32
     for name in ("spt_default_params", "spt_camera_init", "spt_scene_cornell",
                  "spt_scene_spheres32", "spt_render", "spt_context_create",
                  "spt_context_destroy", "spt_context_reserve", "spt_render_async",
@@ -295,9 +316,13 @@ class Renderer:
     def close(self):
         if self._ctx:
             self.lib.spt_context_destroy(self._ctx)
-            self._ctx = ctypes.c_void_p()
+            self._ctx = None
 
-    __del__ = close
+    def __del__(self):  # at interpreter exit module globals (ctypes) may already be gone
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
     def reserve(self, n_prims: int, params: spt_params):
         _check(self.lib.spt_context_reserve(self._ctx, int(n_prims), ctypes.byref(params)))
@@ -316,29 +341,47 @@ class Renderer:
 
 
 # ---------------------------------------------------------------------------------------------
-# Output (:313-321, :548-551)
+# Output (:313-321 toInt/clamp, :548-551 the P3 writer): encoded on the GPU (spt_image.hip)
 # ---------------------------------------------------------------------------------------------
-def clamp(x):
-    return np.clip(x, 0.0, 1.0)
+def _format(fmt) -> int:
+    return IMAGE_FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
 
 
-def toInt(x) -> np.ndarray:
-    """int(pow(clamp(x), 1/2.2)*255 + .5) in double, as :319-321."""
-    x = np.asarray(x, dtype=np.float64)
-    return (np.power(np.clip(x, 0.0, 1.0), 1 / 2.2) * 255 + 0.5).astype(np.int64)
+def write_image(path: str, rgb: np.ndarray, fmt="p3", device: int = 0) -> None:
+    """Write an (h, w, 3) float32 framebuffer as P3 (byte-identical to :548-551), P6 or PFM."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w, _ = a.shape
+    _check(load_library().spt_write_image(device, a.ctypes.data, w, h, _format(fmt),
+                                          path.encode()))
 
 
-def ppm_bytes(rgb: np.ndarray) -> bytes:
-    """ASCII P3 exactly as :549-551: header then '%d %d %d ' per pixel, no newlines."""
-    h, w, _ = rgb.shape
-    vals = toInt(rgb.reshape(-1, 3))
-    body = " ".join(f"{a} {b} {c}" for a, b, c in vals.tolist())
-    return (f"P3\n{w} {h}\n255\n" + body + (" " if len(vals) else "")).encode()
+def write_ppm(path: str, rgb: np.ndarray, device: int = 0) -> None:
+    """The reference's writer (:548-551): ASCII P3, '%d %d %d ' per pixel."""
+    write_image(path, rgb, "p3", device)
 
 
-def write_ppm(path: str, rgb: np.ndarray) -> None:
-    with open(path, "wb") as f:
-        f.write(ppm_bytes(rgb))
+class Encoder:
+    """spt_encoder: device framebuffer -> file bytes in a device buffer (spt_encode_image)."""
+
+    def __init__(self, device: int = 0):
+        self._e = ctypes.c_void_p()
+        _check(load_library().spt_encoder_create(device, ctypes.byref(self._e)))
+
+    def close(self):
+        if self._e:
+            load_library().spt_encoder_destroy(self._e)
+            self._e = None
+
+    @staticmethod
+    def bound(w: int, h: int, fmt="p3") -> int:
+        return int(load_library().spt_image_bound(w, h, _format(fmt)))
+
+    def encode(self, rgb_dev_ptr: int, w: int, h: int, fmt, out_dev_ptr: int, cap: int,
+               stream: int = 0) -> int:
+        n = ctypes.c_uint64()
+        _check(load_library().spt_encode_image(self._e, rgb_dev_ptr, w, h, _format(fmt),
+                                               out_dev_ptr, cap, ctypes.byref(n), stream or None))
+        return int(n.value)
 
 
 def flop_model(stats: dict, prims: Iterable[spt_prim]) -> float:

@@ -101,13 +101,11 @@ inline double clamp(double x) { return x < 0 ? 0 : x > 1 ? 1 : x; }             
 inline int toInt(double x) { return int(std::pow(clamp(x), 1 / 2.2) * 255 + .5); }  // :319-321
 
 // P3 writer :548-551 (byte-identical output; this one also closes the file).
-inline int write_ppm(const char* path, int w, int h, const float* c) {
-  FILE* f = std::fopen(path, "w");
-  if (!f) return 1;
-  std::fprintf(f, "P3\n%d %d\n%d\n", w, h, 255);
-  for (int i = 0; i < w * h; i++)
-    std::fprintf(f, "%d %d %d ", toInt(c[3 * i]), toInt(c[3 * i + 1]), toInt(c[3 * i + 2]));
-  return std::fclose(f);
+// The writer of :548-551 (ASCII P3, "%d %d %d " per pixel, toInt :319-321), encoded on the GPU
+// (spt_write_image): byte-identical to the reference's fprintf loop. P6 / PFM via `format`.
+inline int write_ppm(const char* path, int w, int h, const float* c, int device = 0,
+                     int format = SPT_IMAGE_P3) {
+  return spt_write_image(device, c, w, h, format, path) == SPT_OK ? 0 : 1;
 }
 
 // The drop-in for the pixel loop :528-542: linear clamped RGB, row-major, y=0 top.

