@@ -93,8 +93,13 @@ typedef struct spt_params {
   int32_t shard_index, shard_count;
   int32_t chunk;              /* samples per work unit (0 = auto). Never changes results. */
   int32_t device;             /* HIP device ordinal for spt_render() */
-  uint32_t flags;             /* reserved, must be 0 */
+  uint32_t flags;             /* SPT_FLAG_* below; other bits must be 0 */
 } spt_params;
+
+/* random_scattering() draws from the reference's commented-out UNIFORM hemisphere code (:351-360:
+ * dir = u cos(r1) sqrt(r2(2-r2)) + v sin(r1) sqrt(r2(2-r2)) + w (1-r2)) instead of the live
+ * cosine-weighted code (:340-347); the estimator weight stays 1, as in the reference. */
+#define SPT_FLAG_UNIFORM_SCATTER 1u
 
 /* Philox4x32-10 key (fixed, so the key schedule is compile-time) and counter layout:
  * ctr = (pixel = y*w + x, sample, vertex | stream << 31, seed). */

@@ -13,6 +13,7 @@
 #   :517      skip create_state_space (keeps the rand() stream starting at the pixel loop)
 #   :548      output file name from argv[5]
 #   :464      (cosine variant only) q < 1  ->  q < 0
+#   :340-360  (uniform variant only) cosine body out, the commented uniform hemisphere body in
 # Pinned build: g++ -O3, x86-64 baseline (no -march=native: FMA contraction changes bits).
 set -euo pipefail
 REF=${REF:-/root/reference/src}
@@ -37,4 +38,7 @@ build() {  # $1 = output binary, rest = extra sed expressions
 }
 build smallpt_nee
 build smallpt_cos -e '464s/if (q < 1)/if (q < 0)/'
-echo "built $OUT/smallpt_nee $OUT/smallpt_cos"
+# uniform-hemisphere variant of random_scattering: the live cosine body :340-347 removed and the
+# commented-out uniform body :352-359 enabled (its /* and */ lines :351, :360 removed)
+build smallpt_uni -e '340,347d' -e '351d' -e '360d'
+echo "built $OUT/smallpt_nee $OUT/smallpt_cos $OUT/smallpt_uni"

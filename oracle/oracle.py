@@ -78,12 +78,13 @@ def camera(aspect: float):
     return c
 
 
-def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, prims=None):
+def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, prims=None,
+                  uniform: bool = False):
     """fp64 restatement of the reference (bit-exact with the patched oracle). (h, w, 3) float64."""
     prims = prims or scene_cornell()
     arr = (_spt.spt_prim * len(prims))(*prims)
     out = np.zeros((h, w, 3), dtype=np.float64)
-    lib().spt_oracle_compat_render(arr, len(prims), w, h, spp, seed, int(nee),
+    lib().spt_oracle_compat_render(arr, len(prims), w, h, spp, seed, int(nee) | (2 if uniform else 0),
                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return out
 

@@ -1,3 +1,4 @@
+#define _GNU_SOURCE /* sincos() */
 /*
  * spt_oracle.c — CPU ORACLE for the smallpt per-pixel sampling loop.
  *
@@ -128,7 +129,8 @@ typedef struct {
   const o_prim* prims;
   int n;
   int light_id;
-  int nee; /* 1: `q < 1` (HEAD :464), 0: `q < 0` (cosine-only) */
+  int nee;     /* 1: `q < 1` (HEAD :464), 0: `q < 0` (cosine-only) */
+  int uniform; /* random_scattering: 0 = cosine code :340-347, 1 = uniform code :352-359 */
   o_glibc_rand* g;
 } o_scene;
 
@@ -155,16 +157,30 @@ static dv o_normal(const o_prim* P, dv d, dv x) {
   return ddot(n, d) < 0 ? n : dmul(n, (double)-1); /* n * -1 : Vec::operator*(int) */
 }
 
-/* random_scattering :337-348 (cosine-weighted). */
-static dv o_random_scattering(dv nl, unsigned short* Xi) {
+/* random_scattering :337-361: cosine-weighted (live, :340-347) or the commented-out uniform
+   hemisphere (:352-359, `uniform`). */
+static dv o_random_scattering(dv nl, unsigned short* Xi, int uniform) {
   const double r1 = 2 * M_PI * o_erand48(Xi);
   const double r2 = o_erand48(Xi);
-  const double r2s = sqrt(r2);
   const dv w = nl;
   const dv u = dnorm(dcross(fabs(w.x) > .1 ? dv3(0, 1, 0) : dv3(1, 0, 0), w));
   const dv v = dcross(w, u);
-  return dnorm(dadd(dadd(dmul(dmul(u, cos(r1)), r2s), dmul(dmul(v, sin(r1)), r2s)),
-                    dmul(w, sqrt(1 - r2))));
+  /* libm calls as the reference binary makes them (objdump of oracle/_ref): g++ -O3 turns the
+     cosine body's cos(r1)/sin(r1) into one glibc sincos() call, but keeps separate sin()/cos()
+     calls in the uniform body; glibc's sincos and sin/cos differ in the last bit for some r1. */
+  if (uniform) {
+    double (*volatile cos_f)(double) = cos, (*volatile sin_f)(double) = sin;
+    return dnorm(dadd(dadd(dmul(dmul(u, cos_f(r1)), sqrt(r2 * (2 - r2))),
+                           dmul(dmul(v, sin_f(r1)), sqrt(r2 * (2 - r2)))),
+                      dmul(w, 1 - r2)));
+  }
+  {
+    const double r2s = sqrt(r2);
+    double sr1, cr1;
+    sincos(r1, &sr1, &cr1);
+    return dnorm(dadd(dadd(dmul(dmul(u, cr1), r2s), dmul(dmul(v, sr1), r2s)),
+                      dmul(w, sqrt(1 - r2))));
+  }
 }
 
 /* light_sampling :363-369. rand()*36 is int arithmetic (wraps with glibc RAND_MAX=2^31-1). */
@@ -200,7 +216,7 @@ static dv o_radiance(const o_scene* S, dv ro, dv rd, int depth, unsigned short* 
       d = dnorm(d);
       o_intersect(S, x, d, &t, &id);
       if (id != S->light_id) {
-        d = o_random_scattering(nl, Xi);
+        d = o_random_scattering(nl, Xi, S->uniform);
         d = dnorm(d);
         o_intersect(S, x, d, &t, &id);
       } else {
@@ -210,7 +226,7 @@ static dv o_radiance(const o_scene* S, dv ro, dv rd, int depth, unsigned short* 
         BRDF = fabs(ddot(d, nl) / M_PI);
       }
     } else {
-      d = o_random_scattering(nl, Xi);
+      d = o_random_scattering(nl, Xi, S->uniform);
       d = dnorm(d);
       o_intersect(S, x, d, &t, &id);
     }
@@ -250,6 +266,7 @@ void spt_oracle_camera(double out[12], const double lf[3], const double la[3], c
 }
 
 /* main() :502-542 with the HEAD scene, srand(seed) and the state-space build skipped.
+ * nee: bit 0 = `q < 1` (HEAD) vs `q < 0`; bit 1 = uniform random_scattering (:352-359).
  * c_out: w*h*3 doubles (clamped, row-major, y=0 top). Returns 0. */
 int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp, unsigned seed,
                              int nee, double* c_out) {
@@ -261,7 +278,7 @@ int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp
   int i, y;
   dv origin, llc, hor, ver;
   for (i = 0; i < n; i++) P[i] = o_from_spt(&prims[i]);
-  S.prims = P; S.n = n; S.light_id = 6; S.nee = nee; S.g = &g;
+  S.prims = P; S.n = n; S.light_id = 6; S.nee = nee & 1; S.uniform = (nee >> 1) & 1; S.g = &g;
   o_srand(&g, seed);
   spt_oracle_camera(cam, lf, la, up, 65, (float)w / (float)h);
   origin = dv3(cam[0], cam[1], cam[2]);
@@ -553,14 +570,22 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   return tmin < 1e20f;
 }
 
-static fv c_cosine(fv nl, uint32_t ra, uint32_t rb) {
+/* random_scattering in the contract: cosine (:340-347), or with `uniform` the commented-out
+   uniform hemisphere (:352-359): radial sqrt(r2*(2-r2)) and normal component (1-r2). */
+static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
   const float xi1 = u01(ra), xi2 = u01(rb);
   float s, c;
   fv a, u, v;
   float r2s, s1, cr, sr;
   spt_oracle_sincos2pi(xi1, &s, &c);
-  r2s = xi2 * spt_oracle_rsq_nr(xi2);
-  s1 = (1.0f - xi2) * spt_oracle_rsq_nr(1.0f - xi2);
+  if (uniform) {
+    const float m = xi2 * (2.0f - xi2);
+    r2s = m * spt_oracle_rsq_nr(m);
+    s1 = 1.0f - xi2;
+  } else {
+    r2s = xi2 * spt_oracle_rsq_nr(xi2);
+    s1 = (1.0f - xi2) * spt_oracle_rsq_nr(1.0f - xi2);
+  }
   cr = c * r2s;
   sr = s * r2s;
   if ((nl.y == 0.0f && nl.z == 0.0f && fabsf(nl.x) == 1.0f) ||
@@ -710,11 +735,11 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
           dn = dl;
           carried = 1; c_hit = sh; c_t = ts; c_id = ids;
         } else {
-          dn = c_cosine(nl, r[2], r[3]);
+          dn = c_cosine(nl, r[2], r[3], (P->flags & SPT_FLAG_UNIFORM_SCATTER) != 0);
           st->cosine_samples++;
         }
       } else {
-        dn = c_cosine(nl, r[2], r[3]);
+        dn = c_cosine(nl, r[2], r[3], (P->flags & SPT_FLAG_UNIFORM_SCATTER) != 0);
         st->cosine_samples++;
       }
       L = fv3(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));

@@ -94,6 +94,7 @@ EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_sc
            "spt_status_string", "spt_last_error", "spt_device_count", "spt_image_bound",
            "spt_encoder_create", "spt_encoder_destroy", "spt_encode_image", "spt_write_image"]
 IMAGE_FORMATS = {"p3": 0, "p6": 1, "pfm": 2}
+FLAG_UNIFORM_SCATTER = 1  # spt_params.flags: random_scattering from the uniform code of :352-359
 
 _lib = None
 

@@ -110,14 +110,23 @@ __device__ __forceinline__ void sincos2pi(float xi, float& s_out, float& c_out) 
 // random_scattering :337-347 (cosine-weighted hemisphere about nl), before the final normalize
 // (the kernel shares that normalize with the camera ray, :536). AXIS: nl is known to be
 // axis-aligned (rect-only scenes); otherwise it is tested per lane, as the oracle does.
+// uniform: the reference's commented-out uniform hemisphere (:352-359), radial sqrt(r2(2-r2)) and
+// normal component 1-r2 (SPT_FLAG_UNIFORM_SCATTER; oracle c_cosine).
 template <bool AXIS = false>
-__device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb) {
+__device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool uniform = false) {
   const float xi1 = u01(ra), xi2 = u01(rb);
   float s, c;
   sincos2pi(xi1, s, c);
-  const float r2s = xi2 * rsq_nr(xi2);  // sqrt(r2); xi2 = 0 gives 0
-  const float om = 1.0f - xi2;
-  const float s1 = om * rsq_nr(om);     // sqrt(1 - r2)
+  float r2s, s1;
+  if (uniform) {
+    const float m = xi2 * (2.0f - xi2);
+    r2s = m * rsq_nr(m);
+    s1 = 1.0f - xi2;
+  } else {
+    r2s = xi2 * rsq_nr(xi2);  // sqrt(r2); xi2 = 0 gives 0
+    const float om = 1.0f - xi2;
+    s1 = om * rsq_nr(om);     // sqrt(1 - r2)
+  }
   const float cr = c * r2s, sr = s * r2s;
   // Contract: an axis-aligned normal (every rectangle's, :123,:166,:209) makes the frame of
   // :345-346 a signed permutation of the axes: (sx,0,0) -> (sx*s1, sr, -sx*cr);

@@ -88,6 +88,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // always ends there (RR with p == 0, :448), so the NEE test only needs "is the nearest hit the
   // light" — an occlusion query without id bookkeeping.
   int light_black, light_kind, light_pos;
+  int scatter_uniform;  // SPT_FLAG_UNIFORM_SCATTER
   unsigned long long* accum;  // [n_local_pix][3] 32.32 fixed point
   uint32_t* queue;            // [0] = next unit
   unsigned long long* stats;  // [8]
@@ -403,9 +404,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       f3 v = mk(0, 0, 0);
       if (cont) {
         SPT_REGION(8);
-        v = cosine_vec<!TP::SPH>(nl, r.z, r.w);
+        v = cosine_vec<!TP::SPH>(nl, r.z, r.w, cptr(Pg)->scatter_uniform != 0);
         if (SPT_PROBE & 8) {
-          const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w);
+          const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, cptr(Pg)->scatter_uniform != 0);
           if (opq(0u) != 0u) v = v2;
         }
       }
@@ -682,7 +683,7 @@ static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* c
   if (p->shard_count < 1 || p->shard_index < 0 || p->shard_index >= p->shard_count)
     return fail(SPT_ERR_INVALID_ARG, "bad shard_index/shard_count");
   if (p->tile_rows < 0 || p->chunk < 0) return fail(SPT_ERR_INVALID_ARG, "negative tile/chunk");
-  if (p->flags != 0) return fail(SPT_ERR_INVALID_ARG, "flags must be 0");
+  if (p->flags & ~SPT_FLAG_UNIFORM_SCATTER) return fail(SPT_ERR_INVALID_ARG, "unknown flags");
   if (p->light_mode != SPT_LIGHT_GLIBC_WRAP && p->light_mode != SPT_LIGHT_UNIFORM)
     return fail(SPT_ERR_INVALID_ARG, "bad light_mode");
   if (p->light_mode == SPT_LIGHT_GLIBC_WRAP &&
@@ -914,6 +915,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.light_black = light_pos >= 0 && c->h_prims[p->light_id].pmax == 0.0f ? 1 : 0;
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
+  K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
   c->n_prims = n_prims;
   c->last = K;
   c->samples = (uint64_t)K.n_local_pix * (uint64_t)p->spp;

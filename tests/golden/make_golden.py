@@ -32,12 +32,12 @@ def main():
     subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
     ref = os.path.join(ROOT, "oracle", "_ref")
     out = {"recipe": "oracle/build_ref.sh: sed patch of smallpt.cpp (:424-442 deleted, srand(seed), "
-                     "argv w h spp seed out, :517 skipped; cosine: :464 q<1 -> q<0) | g++ -O3 (x86-64 "
-                     "baseline, g++ 11.4)", "reference_md5": {}}
+                     "argv w h spp seed out, :517 skipped; cosine: :464 q<1 -> q<0; uni: :340-347 out, "
+                     ":351/:360 comment markers out) | g++ -O3 (x86-64 baseline, g++ 11.4)", "reference_md5": {}}
     tmp = "/tmp/spt_golden"
     os.makedirs(tmp, exist_ok=True)
     for w, h, spp in ((64, 48, 4), (256, 192, 4)):
-        for est in ("nee", "cos"):
+        for est in ("nee", "cos", "uni"):
             path = os.path.join(tmp, f"ref_{w}x{h}_s{spp}_{est}.ppm")
             subprocess.run([os.path.join(ref, f"smallpt_{est}"), str(w), str(h), str(spp), "1", path],
                            check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
@@ -69,10 +69,11 @@ def main():
     o.build()
     prims = o.scene_cornell()
     out["counter_md5"] = {}
-    for est, q in (("nee", 1.0), ("cos", 0.0)):
-        p = o.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q)
+    for est, q, fl in (("nee", 1.0, 0), ("cos", 0.0, 0), ("uni", 1.0, 1)):
+        p = o.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
         img, st = o.counter_render(prims, o.camera(64 / 48), p)
-        np.save(os.path.join(HERE, f"counter_64x48_s16_{est}.npy"), img)
+        if est != "uni":
+            np.save(os.path.join(HERE, f"counter_64x48_s16_{est}.npy"), img)
         out["counter_md5"][est] = hashlib.md5(img.tobytes()).hexdigest()
         out.setdefault("counter_stats", {})[est] = st
     with open(os.path.join(HERE, "golden.json"), "w") as f:

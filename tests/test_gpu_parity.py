@@ -33,9 +33,10 @@ def _assert_exact(gpu, cpu):
     assert diff.size == 0, f"{len(diff)} mismatching values, first {diff[:5].tolist()}, rmse {rmse}"
 
 
-@pytest.mark.parametrize("est,q", [("nee", 1.0), ("cos", 0.0)])
-def test_small_image_bit_exact_and_stats(spt, oracle, est, q):
-    p = spt.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q)
+@pytest.mark.parametrize("est,q,fl", [("nee", 1.0, 0), ("cos", 0.0, 0), ("uni", 1.0, 1)])
+def test_small_image_bit_exact_and_stats(spt, oracle, est, q, fl):
+    """uni: HEAD with the uniform-hemisphere random_scattering of :352-359 (SPT_FLAG_UNIFORM_SCATTER)."""
+    p = spt.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
     gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
     _assert_exact(gpu, cpu)
     assert hashlib.md5(gpu.tobytes()).hexdigest() == GOLD["counter_md5"][est]
@@ -52,6 +53,7 @@ def test_small_image_bit_exact_and_stats(spt, oracle, est, q):
     dict(width=40, height=30, spp=6, seed=6, max_depth=3),          # hard depth cap
     dict(width=40, height=30, spp=6, seed=7, rr_depth=0),           # RR from the first vertex
     dict(width=1, height=1, spp=64, seed=8),                        # single pixel
+    dict(width=40, height=30, spp=6, seed=10, nee_prob=0.0, flags=1),  # uniform hemisphere only
 ])
 def test_edge_cases_bit_exact(spt, oracle, case):
     p = spt.default_params(**case)
@@ -60,8 +62,9 @@ def test_edge_cases_bit_exact(spt, oracle, case):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
-def test_sphere_scene_bit_exact(spt, oracle):
-    p = spt.default_params(width=48, height=48, spp=8, seed=3, max_depth=16)
+@pytest.mark.parametrize("fl", [0, 1])
+def test_sphere_scene_bit_exact(spt, oracle, fl):
+    p = spt.default_params(width=48, height=48, spp=8, seed=3, max_depth=16, flags=fl)
     gpu, gst, cpu, cst = _render_both(spt, oracle, spt.spheres32_scene(), p)
     _assert_exact(gpu, cpu)
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst

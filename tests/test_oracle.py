@@ -26,17 +26,18 @@ def _md5_of_ppm(oracle, img, tmp_path, name):
     return hashlib.md5(open(path, "rb").read()).hexdigest()
 
 
-@pytest.mark.parametrize("w,h,est", [(64, 48, "nee"), (64, 48, "cos"), (256, 192, "nee"),
-                                     (256, 192, "cos")])
+@pytest.mark.parametrize("w,h,est", [(64, 48, "nee"), (64, 48, "cos"), (64, 48, "uni"),
+                                     (256, 192, "nee"), (256, 192, "cos"), (256, 192, "uni")])
 def test_compat_restatement_matches_reference_md5(oracle, tmp_path, w, h, est):
-    img = oracle.compat_render(w, h, 4, seed=1, nee=(est == "nee"))
+    """est: nee = HEAD; cos = :464 q<0; uni = HEAD with the uniform hemisphere of :352-359."""
+    img = oracle.compat_render(w, h, 4, seed=1, nee=(est != "cos"), uniform=(est == "uni"))
     assert _md5_of_ppm(oracle, img, tmp_path, "c.ppm") == GOLD["reference_md5"][f"{w}x{h}_s4_seed1_{est}"]
 
 
-@pytest.mark.parametrize("est", ["nee", "cos"])
+@pytest.mark.parametrize("est", ["nee", "cos", "uni"])
 def test_reference_ppm_fixture_matches(oracle, tmp_path, est):
     """The committed reference PPM (data) equals the restatement's bytes."""
-    img = oracle.compat_render(64, 48, 4, seed=1, nee=(est == "nee"))
+    img = oracle.compat_render(64, 48, 4, seed=1, nee=(est != "cos"), uniform=(est == "uni"))
     path = str(tmp_path / "c.ppm")
     oracle.write_ppm(path, img)
     assert open(path, "rb").read() == open(os.path.join(HERE, "golden", f"ref_64x48_s4_{est}.ppm"), "rb").read()
@@ -47,12 +48,12 @@ def test_reference_ppm_fixture_matches(oracle, tmp_path, est):
 @pytest.mark.parametrize("seed,w,h,spp", [(7, 40, 30, 3), (123, 33, 17, 5)])
 def test_compat_restatement_matches_reference_binary_other_seeds(oracle, tmp_path, seed, w, h, spp):
     """Beyond the committed md5s: odd sizes and other seeds against the live reference binary."""
-    for est in ("nee", "cos"):
+    for est in ("nee", "cos", "uni"):
         ref_path = str(tmp_path / f"ref_{est}.ppm")
         subprocess.run([os.path.join(REF_DIR, f"smallpt_{est}"), str(w), str(h), str(spp), str(seed),
                         ref_path], check=True, cwd=str(tmp_path), stdout=subprocess.DEVNULL,
                        stderr=subprocess.DEVNULL)
-        img = oracle.compat_render(w, h, spp, seed=seed, nee=(est == "nee"))
+        img = oracle.compat_render(w, h, spp, seed=seed, nee=(est != "cos"), uniform=(est == "uni"))
         assert _md5_of_ppm(oracle, img, tmp_path, "c.ppm") == hashlib.md5(open(ref_path, "rb").read()).hexdigest()
 
 
@@ -124,8 +125,8 @@ def test_light_sampling_wraps_like_glibc(oracle):
 def test_counter_mode_pins(oracle):
     """The counter-mode contract (what the GPU must match) is stable: committed images/md5s."""
     prims = oracle.scene_cornell()
-    for est, q in (("nee", 1.0), ("cos", 0.0)):
-        p = oracle.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q)
+    for est, q, fl in (("nee", 1.0, 0), ("cos", 0.0, 0), ("uni", 1.0, 1)):
+        p = oracle.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
         img, st = oracle.counter_render(prims, oracle.camera(64 / 48), p)
         assert hashlib.md5(img.tobytes()).hexdigest() == GOLD["counter_md5"][est]
         assert st == GOLD["counter_stats"][est]
