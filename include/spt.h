@@ -128,6 +128,9 @@ spt_status spt_camera_init(spt_camera* cam, const double lookfrom[3], const doub
 spt_status spt_scene_cornell(spt_prim* out, int32_t cap, int32_t* n_out);
 /* The build-defined 32-sphere scene of config 5: room rects 0-6 of :288-294 + 32 DIFF spheres. */
 spt_status spt_scene_spheres32(spt_prim* out, int32_t cap, int32_t* n_out);
+/* The room and light of :288-294 plus smallpt's mirror (SPEC) and glass (REFR) balls at the places
+ * of the spheres commented out at :296-297; shading = the commented-out code :481-495. 9 prims. */
+spt_status spt_scene_cornell_specular(spt_prim* out, int32_t cap, int32_t* n_out);
 /* Rows rendered by this shard (params tile_rows/shard_index/shard_count), ascending. Returns count. */
 int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
 

@@ -500,6 +500,7 @@ typedef struct {
   float rad2, px, py, pz;  /* sphere */
   fv e, c;
   float pmax;
+  int refl;                /* spt_refl: DIFF, SPEC, REFR */
 } c_prim;
 
 /* Rect bounds [lo, hi] of :106 as |a - mid| <= half with mid = (lo+hi)/2, half = (hi-lo)/2
@@ -613,13 +614,23 @@ typedef struct {
       misses;
 } c_stats;
 
+/* A pending REFR branch (:494-495 at depth <= 2 returns reflection*Re + refraction*Tr): the
+   refraction child is traced after the reflection subtree (depth-first), into the same L. */
+typedef struct {
+  fv o, d, T;
+  int depth;
+  uint32_t branch;
+} c_node;
+
 /* One path of the counter-mode contract; returns L. */
 static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const float cam[12],
                  c_stats* st) {
   const spt_params* P = C->P;
   uint32_t ctr[4], r[4], rl[4];
   fv o, d, T = fv3(1, 1, 1), L = fv3(0, 0, 0);
-  int depth = 0, carried = 0, c_hit = 0, c_id = 0;
+  int depth = 0, carried = 0, c_hit = 0, c_id = 0, sp = 0;
+  uint32_t branch = 0; /* path-tree position: bit k-1 set = refraction child of the split at depth k */
+  c_node stack[2];
   float c_t = 0;
   /* Camera ray :533-536. The jitter comes from the low bytes of vertex 1's Philox call (16 bits
    * each), so a sample start costs no extra RNG call; 1/w, 1/h are rounded once. */
@@ -638,7 +649,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
   for (;;) {
     int id = 0, hit;
     float t;
-    fv x, nl, f, e;
+    fv x, nl, gn, f, e;
     const c_prim* H;
     if (carried) {
       hit = c_hit; t = c_t; id = hit ? c_id : 0;
@@ -660,13 +671,13 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
       x = fv3(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
     }
     st->vertices++;
-    switch (H->kind) {
-      case SPT_RECT_XY: nl = d.z < 0.0f ? fv3(0, 0, 1) : fv3(0, 0, -1); break;
-      case SPT_RECT_XZ: nl = d.y < 0.0f ? fv3(0, 1, 0) : fv3(0, -1, 0); break;
-      case SPT_RECT_YZ: nl = d.x < 0.0f ? fv3(1, 0, 0) : fv3(-1, 0, 0); break;
+    switch (H->kind) { /* gn: the unoriented (geometric) normal `n` of :482-491 */
+      case SPT_RECT_XY: nl = d.z < 0.0f ? fv3(0, 0, 1) : fv3(0, 0, -1); gn = fv3(0, 0, 1); break;
+      case SPT_RECT_XZ: nl = d.y < 0.0f ? fv3(0, 1, 0) : fv3(0, -1, 0); gn = fv3(0, 1, 0); break;
+      case SPT_RECT_YZ: nl = d.x < 0.0f ? fv3(1, 0, 0) : fv3(-1, 0, 0); gn = fv3(1, 0, 0); break;
       default: {
-        const fv n = fnormalize(fv3(x.x - H->px, x.y - H->py, x.z - H->pz));
-        nl = fdot(n, d) < 0.0f ? n : fv3(-n.x, -n.y, -n.z);
+        gn = fnormalize(fv3(x.x - H->px, x.y - H->py, x.z - H->pz));
+        nl = fdot(gn, d) < 0.0f ? gn : fv3(-gn.x, -gn.y, -gn.z);
       }
     }
     f = H->c;
@@ -676,7 +687,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
      * the low bytes form a 16-bit RR draw (r0, r1) and a 16-bit NEE-mix draw (r2, r3) — except at
      * vertex 1, whose low bytes were the camera jitter: its RR / NEE-mix draws (only needed when
      * rr_depth < 1 or 0 < nee_prob < 1) come from stream 1. */
-    ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth; ctr[3] = P->seed;
+    ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth | (branch << 24); ctr[3] = P->seed;
     spt_oracle_philox(ctr, C->key, r);
     rl[0] = r[0]; rl[1] = r[1]; rl[2] = r[2]; rl[3] = r[3];
     if (depth == 1) {
@@ -700,8 +711,53 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
       }
       if (term) {
         L = fv3(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+        if (sp > 0) { /* the pending refraction child of a REFR split */
+          --sp;
+          o = stack[sp].o; d = stack[sp].d; T = stack[sp].T;
+          depth = stack[sp].depth; branch = stack[sp].branch;
+          continue;
+        }
         return L;
       }
+    }
+    if (H->refl != SPT_DIFF) {
+      /* SPEC :481-482 and REFR :484-495 (smallpt's commented-out code, fp32): no NEE; the RR of
+         :448 above already ran. reflRay direction r.d - n*2*n.dot(r.d), not renormalised. */
+      const fv Tf = fv3(T.x * f.x, T.y * f.y, T.z * f.z);
+      const float k2 = 2.0f * fdot(gn, d);
+      const fv refl = fv3(d.x - gn.x * k2, d.y - gn.y * k2, d.z - gn.z * k2);
+      L = fv3(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+      o = x;
+      T = Tf;
+      if (H->refl == SPT_REFR) {
+        const int into = fdot(gn, nl) > 0.0f;                       /* :485 */
+        const float nnt = into ? 1.0f / 1.5f : 1.5f / 1.0f;          /* nc=1, nt=1.5 :486 */
+        const float ddn = fdot(d, nl);
+        const float cos2t = 1.0f - nnt * nnt * (1.0f - ddn * ddn);
+        if (!(cos2t < 0.0f)) {                                       /* else TIR :487-488 */
+          const float kk = (into ? 1.0f : -1.0f) * (ddn * nnt + sqrtf(cos2t));
+          const fv tdir = fnormalize(fv3(d.x * nnt - gn.x * kk, d.y * nnt - gn.y * kk,
+                                         d.z * nnt - gn.z * kk));   /* :489 */
+          const float a = 1.5f - 1.0f, b = 1.5f + 1.0f, R0 = a * a / (b * b);
+          const float c = 1.0f - (into ? -ddn : fdot(tdir, gn));
+          const float Re = R0 + (1.0f - R0) * c * c * c * c * c, Tr = 1.0f - Re;
+          const float Pp = 0.25f + 0.5f * Re, RP = Re / Pp, TP = Tr / (1.0f - Pp);  /* :491 */
+          if (depth > 2) { /* Russian roulette between the two :492-493 */
+            if (u16(rl[2], rl[3]) < Pp) { T = fv3(Tf.x * RP, Tf.y * RP, Tf.z * RP); d = refl; }
+            else { T = fv3(Tf.x * TP, Tf.y * TP, Tf.z * TP); d = tdir; }
+          } else { /* both :494-495: reflection now, refraction later */
+            stack[sp].o = x; stack[sp].d = tdir;
+            stack[sp].T = fv3(Tf.x * Tr, Tf.y * Tr, Tf.z * Tr);
+            stack[sp].depth = depth; stack[sp].branch = branch | (1u << (depth - 1));
+            ++sp;
+            T = fv3(Tf.x * Re, Tf.y * Re, Tf.z * Re);
+            d = refl;
+          }
+          continue;
+        }
+      }
+      d = refl;
+      continue;
     }
     {
       int nee;
@@ -775,6 +831,7 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
     P->e = fv3((float)s[i].e[0], (float)s[i].e[1], (float)s[i].e[2]);
     P->c = fv3((float)s[i].c[0], (float)s[i].c[1], (float)s[i].c[2]);
     P->pmax = P->c.x > P->c.y && P->c.x > P->c.z ? P->c.x : P->c.y > P->c.z ? P->c.y : P->c.z;
+    P->refl = s[i].refl;
   }
 }
 

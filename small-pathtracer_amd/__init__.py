@@ -89,6 +89,7 @@ STAT_KEYS = ["samples", "path_rays", "shadow_rays", "vertices", "nee_events", "n
 
 # Every entry point declared in include/spt.h (checked by tests/test_capi.py).
 EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_scene_spheres32",
+           "spt_scene_cornell_specular",
            "spt_shard_rows", "spt_render", "spt_context_create", "spt_context_destroy",
            "spt_context_reserve", "spt_render_async", "spt_context_stats", "spt_abi_version",
            "spt_status_string", "spt_last_error", "spt_device_count", "spt_image_bound",
@@ -121,6 +122,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                     P(ctypes.c_double), ctypes.c_float, ctypes.c_float]
     lib.spt_scene_cornell.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_scene_spheres32.argtypes = [P(spt_prim), I32, P(I32)]
+    lib.spt_scene_cornell_specular.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_shard_rows.argtypes = [P(spt_params), P(I32), I32]
     lib.spt_shard_rows.restype = I32
     lib.spt_render.argtypes = [P(spt_prim), I32, P(spt_camera), P(spt_params),
@@ -148,7 +150,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                  "spt_write_image"):
         getattr(lib, name).restype = I32
     for name in ("spt_default_params", "spt_camera_init", "spt_scene_cornell",
-                 "spt_scene_spheres32", "spt_render", "spt_context_create",
+                 "spt_scene_spheres32", "spt_scene_cornell_specular", "spt_render", "spt_context_create",
                  "spt_context_destroy", "spt_context_reserve", "spt_render_async",
                  "spt_context_stats"):
         getattr(lib, name).restype = I32
@@ -263,6 +265,15 @@ def spheres32_scene() -> list:
     arr = (spt_prim * 64)()
     n = ctypes.c_int32()
     _check(lib.spt_scene_spheres32(arr, 64, ctypes.byref(n)))
+    return [arr[i] for i in range(n.value)]
+
+
+def cornell_specular_scene() -> list:
+    """Room + light of :288-294 with smallpt's mirror (SPEC) and glass (REFR) balls (:296-297)."""
+    lib = load_library()
+    arr = (spt_prim * 16)()
+    n = ctypes.c_int32()
+    _check(lib.spt_scene_cornell_specular(arr, 16, ctypes.byref(n)))
     return [arr[i] for i in range(n.value)]
 
 

@@ -97,6 +97,15 @@ inline std::vector<spt_prim> cornell_scene() {  // rect[] :287-311
   };
 }
 
+// The HEAD room and light (:288-294) with smallpt's Mirr/Glas balls at :296-297 (SPEC / REFR).
+inline std::vector<spt_prim> cornell_specular_scene() {
+  std::vector<spt_prim> s = cornell_scene();
+  s.resize(7);
+  s.push_back(Sphere(16.5, Vec(27, 16.5, 47), Vec(), Vec(1, 1, 1) * .999, SPEC));  // Mirr
+  s.push_back(Sphere(16.5, Vec(73, 16.5, 78), Vec(), Vec(1, 1, 1) * .999, REFR));  // Glas
+  return s;
+}
+
 inline double clamp(double x) { return x < 0 ? 0 : x > 1 ? 1 : x; }                 // :314-316
 inline int toInt(double x) { return int(std::pow(clamp(x), 1 / 2.2) * 255 + .5); }  // :319-321
 

@@ -123,6 +123,30 @@ extern "C" spt_status spt_scene_spheres32(spt_prim* o, int32_t cap, int32_t* n_o
   return SPT_OK;
 }
 
+// smallpt's mirror and glass balls in the HEAD room: the room and light of :288-294 (light stays
+// index 6) plus the two spheres commented out at :296-297 with smallpt's materials (Sphere
+// (16.5, (27,16.5,47), c .999, SPEC) "Mirr" and (16.5, (73,16.5,78), c .999, REFR) "Glas"), whose
+// shading is the commented-out SPEC/REFR code :481-495.
+extern "C" spt_status spt_scene_cornell_specular(spt_prim* o, int32_t cap, int32_t* n_out) {
+  if (!o || !n_out || cap < 9) return SPT_ERR_INVALID_ARG;
+  int32_t n17 = 0;
+  spt_prim room[17];
+  spt_scene_cornell(room, 17, &n17);
+  for (int i = 0; i < 7; ++i) o[i] = room[i];
+  const double ctr[2][3] = {{27, 16.5, 47}, {73, 16.5, 78}};
+  for (int k = 0; k < 2; ++k) {
+    spt_prim* p = &o[7 + k];
+    std::memset(p, 0, sizeof *p);
+    p->kind = SPT_SPHERE;
+    p->refl = k == 0 ? SPT_SPEC : SPT_REFR;
+    p->geom[0] = 16.5;
+    p->geom[1] = ctr[k][0]; p->geom[2] = ctr[k][1]; p->geom[3] = ctr[k][2];
+    p->c[0] = p->c[1] = p->c[2] = .999;
+  }
+  *n_out = 9;
+  return SPT_OK;
+}
+
 // Row-tile sharding: tile t (rows [t*T, t*T+T)) belongs to shard t % shard_count; a shard's rows
 // are listed in increasing order (the order of its compact output buffer).
 extern "C" int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap) {

@@ -47,7 +47,9 @@ constexpr uint32_t kMaxWaveIters = 1u << 26;  // [0,8) path stats, [8,28) region
 // axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
 struct alignas(16) DevPrim {
   int kind;
-  float w1, w2, w3, w4, w5, pad0, pad1;
+  float w1, w2, w3, w4, w5;
+  int refl;  // spt_refl
+  float pad1;
   float ex, ey, ez, pmax;
   float cx, cy, cz, pad2;
 };
@@ -119,10 +121,11 @@ struct CornellRectPtr {
 // Scene topology the kernel is specialised for: rect counts per kind (-1 = runtime loop), whether
 // spheres exist (runtime loop), the light's grouped position (-1 = runtime), and whether the rect
 // bounds are the compile-time HEAD scene (CONSTGEO) or read from the uploaded scene (s_load).
+// MAT: SPEC/REFR materials may occur (generic kernel); the specialisations are all-DIFF scenes.
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
-  static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_;
+  static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = SPH_;
 };
 using TopoCornell = Topo<6, 5, 6, false, 8>;     // rect[] of :287-311 (light = XZ #3 -> pos 8)
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
@@ -302,6 +305,10 @@ template <class TP>
 __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
+  // Pending REFR refraction children (:494-495 at depth <= 2), two per lane at most (MAT only):
+  // o, d, T, depth, branch.
+  struct Node { float o[3], d[3], T[3]; int depth; uint32_t branch; };
+  __shared__ Node s_stack[TP::MAT ? kBlock * 2 : 1];
   {
     const SPT_CONST KParams* P = cptr(Pg);
     const SPT_CONST SceneGeo* G = cptr(P->geo);
@@ -319,6 +326,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   bool gen = false;       // needs a new path ray: camera (cont == false) or cosine continuation
   bool cont = false;
   bool shadow = false;    // the pending ray is a NEE shadow ray from vertex o
+  bool spec = false;      // the continuation direction is already set (SPEC/REFR, MAT only)
+  uint32_t branch = 0;    // path-tree position of a REFR split (counter word 2 bits 24+; MAT only)
+  int sp = 0;             // pending refraction children in s_stack (MAT only)
   uint32_t lp = 0, s = 0, s_end = 0, pix = 0;
   int px = 0, py = 0, depth = 0, vid = 0;
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
@@ -392,7 +402,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       need = __ballot(needs_unit);
     }
     if (__ballot(has_unit) == 0) break;
-    n_cos += (uint32_t)__popcll(__ballot(gen && cont));
+    n_cos += (uint32_t)__popcll(__ballot(gen && cont && !(TP::MAT && spec)));
     // per-lane events of this iteration, counted by ballot at its end
     bool e_vert = false, e_miss = false, e_nee = false, e_hit = false;
 
@@ -402,7 +412,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     //    vertex the ray leads to, one normalize for both.
     if (gen) {
       f3 v = mk(0, 0, 0);
-      if (cont) {
+      if (cont && !(TP::MAT && spec)) {
         SPT_REGION(8);
         v = cosine_vec<!TP::SPH>(nl, r.z, r.w, cptr(Pg)->scatter_uniform != 0);
         if (SPT_PROBE & 8) {
@@ -410,7 +420,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           if (opq(0u) != 0u) v = v2;
         }
       }
-      r = philox4x32_10(pix, s, cont ? (uint32_t)depth + 1u : 1u, cptr(Pg)->seed);
+      const uint32_t bw = TP::MAT ? branch << 24 : 0u;
+      r = philox4x32_10(pix, s, (cont ? (uint32_t)depth + 1u : 1u) | bw, cptr(Pg)->seed);
       if (SPT_PROBE & 1) {
         const u4 r2 = philox4x32_10(opq(pix), s, cont ? (uint32_t)depth + 1u : 1u, cptr(Pg)->seed);
         if (opq(0u) != 0u) r = r2;
@@ -428,9 +439,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         L = mk(0, 0, 0);
         depth = 0;
       }
-      d = normalize3(v);
+      if (!(TP::MAT && spec)) d = normalize3(v);
       shadow = false;
       gen = false;
+      spec = false;
     }
 
     n_path += (uint32_t)__popcll(__ballot(has_unit && !shadow));
@@ -464,7 +476,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
           // random draw; anything else is shaded with that vertex's own Philox words.
           if (!(hit && s_prims[id].pmax == 0.0f))
-            r = philox4x32_10(pix, s, (uint32_t)depth + 1u, D->seed);
+            r = philox4x32_10(pix, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u), D->seed);
           vertex = true;
         } else {
           gen = true;  // occluded: continue with the cosine sample (:468-469), T = T*f
@@ -490,13 +502,22 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           else if (kind == SPT_RECT_YZ) tr = (H.w1 - o.x) / d.x;
           x = mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
         }
-        // Hitable::normal, oriented against the ray (:123,:166,:209,:251)
-        if (kind == SPT_RECT_XY) nl = d.z < 0.0f ? mk(0, 0, 1) : mk(0, 0, -1);
-        else if (kind == SPT_RECT_XZ) nl = d.y < 0.0f ? mk(0, 1, 0) : mk(0, -1, 0);
-        else if (kind == SPT_RECT_YZ) nl = d.x < 0.0f ? mk(1, 0, 0) : mk(-1, 0, 0);
-        else {
+        // Hitable::normal, oriented against the ray (:123,:166,:209,:251); gn = the unoriented
+        // (geometric) normal `n` of the SPEC/REFR code :482-491 (MAT only)
+        f3 gn = mk(0, 0, 0);
+        if (kind == SPT_RECT_XY) {
+          nl = d.z < 0.0f ? mk(0, 0, 1) : mk(0, 0, -1);
+          if (TP::MAT) gn = mk(0, 0, 1);
+        } else if (kind == SPT_RECT_XZ) {
+          nl = d.y < 0.0f ? mk(0, 1, 0) : mk(0, -1, 0);
+          if (TP::MAT) gn = mk(0, 1, 0);
+        } else if (kind == SPT_RECT_YZ) {
+          nl = d.x < 0.0f ? mk(1, 0, 0) : mk(-1, 0, 0);
+          if (TP::MAT) gn = mk(1, 0, 0);
+        } else {
           const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
+          if (TP::MAT) gn = n;
         }
         f3 f = mk(H.cx, H.cy, H.cz);
         const f3 e = mk(H.ex, H.ey, H.ez);
@@ -527,7 +548,53 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           }
         }
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
-        if (!term) {
+        if (TP::MAT && !term && H.refl != SPT_DIFF) {
+          // SPEC :481-482 and REFR :484-495 (smallpt's commented-out code; oracle c_path): no NEE.
+          // reflRay direction r.d - n*2*n.dot(r.d), not renormalised.
+          const f3 Tf = mk(T.x * f.x, T.y * f.y, T.z * f.z);
+          const float k2 = 2.0f * dot3(gn, d);
+          const f3 refl = mk(d.x - gn.x * k2, d.y - gn.y * k2, d.z - gn.z * k2);
+          o = x;
+          T = Tf;
+          bool use_refl = true;
+          if (H.refl == SPT_REFR) {
+            const bool into = dot3(gn, nl) > 0.0f;                 // :485
+            const float nnt = into ? 1.0f / 1.5f : 1.5f / 1.0f;    // nc = 1, nt = 1.5 :486
+            const float ddn = dot3(d, nl);
+            const float cos2t = 1.0f - nnt * nnt * (1.0f - ddn * ddn);
+            if (!(cos2t < 0.0f)) {                                 // else total internal reflection
+              const float kk = (into ? 1.0f : -1.0f) * (ddn * nnt + sqrtf(cos2t));
+              const f3 tdir = normalize3(mk(d.x * nnt - gn.x * kk, d.y * nnt - gn.y * kk,
+                                            d.z * nnt - gn.z * kk));  // :489
+              const float a = 1.5f - 1.0f, b = 1.5f + 1.0f, R0 = a * a / (b * b);
+              const float c = 1.0f - (into ? -ddn : dot3(tdir, gn));
+              const float Re = R0 + (1.0f - R0) * c * c * c * c * c, Tr = 1.0f - Re;
+              const float Pp = 0.25f + 0.5f * Re, RP = Re / Pp, TP_ = Tr / (1.0f - Pp);  // :491
+              if (depth > 2) {  // Russian roulette between the two :492-493
+                if (u16(rl.z, rl.w) < Pp) {
+                  T = mk(Tf.x * RP, Tf.y * RP, Tf.z * RP);
+                } else {
+                  T = mk(Tf.x * TP_, Tf.y * TP_, Tf.z * TP_);
+                  d = tdir;
+                  use_refl = false;
+                }
+              } else {  // both :494-495: reflection now, the refraction child later (same L)
+                Node& N = s_stack[threadIdx.x * 2 + sp];
+                N.o[0] = x.x; N.o[1] = x.y; N.o[2] = x.z;
+                N.d[0] = tdir.x; N.d[1] = tdir.y; N.d[2] = tdir.z;
+                N.T[0] = Tf.x * Tr; N.T[1] = Tf.y * Tr; N.T[2] = Tf.z * Tr;
+                N.depth = depth;
+                N.branch = branch | (1u << (depth - 1));
+                ++sp;
+                T = mk(Tf.x * Re, Tf.y * Re, Tf.z * Re);
+              }
+            }
+          }
+          if (use_refl) d = refl;
+          gen = true;
+          cont = true;
+          spec = true;
+        } else if (!term) {
           // DIFF :457-480. T becomes T*f now; the NEE weight (if the light is reached) multiplies
           // it when the shadow ray resolves, so T = (T*f)*w exactly as the contract rounds it.
           T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
@@ -567,7 +634,18 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         }
       }
       // 7) path end: accumulate this sample (:536-538) and start the next one.
-      if (term) {
+      if (TP::MAT && term && sp > 0) {  // the pending refraction child of a REFR split
+        --sp;
+        const Node& N = s_stack[threadIdx.x * 2 + sp];
+        o = mk(N.o[0], N.o[1], N.o[2]);
+        d = mk(N.d[0], N.d[1], N.d[2]);
+        T = mk(N.T[0], N.T[1], N.T[2]);
+        depth = N.depth;
+        branch = N.branch;
+        gen = true;
+        cont = true;
+        spec = true;
+      } else if (term) {
         SPT_REGION(9);
         const float inv_spp = cptr(Pg)->inv_spp;
         acc0 += fix31(L.x, inv_spp);
@@ -576,6 +654,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         ++s;
         gen = true;
         cont = false;
+        if (TP::MAT) branch = 0;
       }
     }
     n_vert += (uint32_t)__popcll(__ballot(e_vert));
@@ -692,8 +771,8 @@ static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* c
   for (int i = 0; i < n; ++i) {
     if (prims[i].kind < SPT_RECT_XY || prims[i].kind > SPT_SPHERE)
       return fail(SPT_ERR_INVALID_ARG, "bad primitive kind");
-    if (prims[i].refl != SPT_DIFF)
-      return fail(SPT_ERR_UNSUPPORTED, "only DIFF materials are live in the reference (:457)");
+    if (prims[i].refl < SPT_DIFF || prims[i].refl > SPT_REFR)
+      return fail(SPT_ERR_INVALID_ARG, "bad material");
   }
   return SPT_OK;
 }
@@ -715,6 +794,7 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
     P.ex = (float)s[i].e[0]; P.ey = (float)s[i].e[1]; P.ez = (float)s[i].e[2];
     P.cx = (float)s[i].c[0]; P.cy = (float)s[i].c[1]; P.cz = (float)s[i].c[2];
     P.pmax = P.cx > P.cy && P.cx > P.cz ? P.cx : P.cy > P.cz ? P.cy : P.cz;  // :447
+    P.refl = s[i].refl;
     out[i] = P;
   }
 }
@@ -932,7 +1012,10 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // Topology specialisation: the HEAD Cornell box (6 XY, 5 XZ, 6 YZ rects, light at grouped
   // position 8) runs a fully unrolled intersect; anything else the generic loops.
   const SceneGeo& g = *c->h_geo;
-  const bool cornell = g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
+  bool all_diff = true;
+  for (int i = 0; i < n_prims; ++i) all_diff = all_diff && prims[i].refl == SPT_DIFF;
+  const bool cornell = all_diff && g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 &&
+                       light_pos == 8;
   static const bool no_const = std::getenv("SPT_NO_CONST_SCENE") != nullptr;  // A/B switch
   const bool cconst = !no_const && cornell_const_match(g, light_pos);
   const int grid = c->n_cu * (cconst    ? c->blocks_per_cu_const

@@ -86,10 +86,13 @@ def test_invalid_arguments_fail_loudly(spt):
         spt.render(spt.cornell_scene(), cam, spt.default_params(width=0))
     assert e.value.status == 1
     bad = spt.cornell_scene()
-    bad[3].refl = spt.SPEC
+    bad[3].refl = 7  # not a Refl_t (:72-74)
     with pytest.raises(spt.SptError) as e:
         spt.render(bad, cam, spt.default_params(width=8, height=8, spp=1))
-    assert e.value.status == 5
+    assert e.value.status == 1
+    with pytest.raises(spt.SptError) as e:
+        spt.render(spt.cornell_scene(), cam, spt.default_params(width=8, height=8, spp=1, flags=4))
+    assert e.value.status == 1
 
 
 def test_no_device_is_an_error_not_a_fallback(spt):

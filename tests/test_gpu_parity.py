@@ -70,6 +70,20 @@ def test_sphere_scene_bit_exact(spt, oracle, fl):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+@pytest.mark.parametrize("case", [
+    dict(width=48, height=36, spp=8, seed=11),                     # mirror + glass, NEE (HEAD)
+    dict(width=40, height=30, spp=6, seed=12, nee_prob=0.0),       # cosine only
+    dict(width=32, height=24, spp=5, seed=13, max_depth=4),        # depth cap inside the splits
+    dict(width=32, height=24, spp=5, seed=14, rr_depth=0, flags=1),  # RR from vertex 1, uniform
+])
+def test_specular_refractive_scene_bit_exact(spt, oracle, case):
+    """SPEC/REFR (:481-495) incl. the depth<=2 reflection+refraction split (per-lane stack)."""
+    p = spt.default_params(**case)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_specular_scene(), p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
 def test_chunk_size_never_changes_results(spt):
     cam = spt.Camera(aspect=40 / 30)
     imgs = [spt.render(spt.cornell_scene(), cam, spt.default_params(width=40, height=30, spp=24, chunk=c))
