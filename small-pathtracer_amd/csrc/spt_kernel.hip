@@ -85,6 +85,9 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   int tile_rows, shard_index, shard_count;
   int chunk, n_local_pix;
   uint32_t n_units;
+  // n / d = (n * m) >> sh for every n < 2^31 (Granlund-Montgomery, host-computed): the refill's
+  // divisions by n_local_pix, width and tile_rows without the ~25-instruction integer divide.
+  uint32_t m_npix, sh_npix, m_w, sh_w, m_tile, sh_tile;
   float inv_spp, inv_w, inv_h;
   // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
   // always ends there (RR with p == 0, :448), so the NEE test only needs "is the nearest hit the
@@ -121,7 +124,8 @@ struct CornellRectPtr {
 // Scene topology the kernel is specialised for: rect counts per kind (-1 = runtime loop), whether
 // spheres exist (runtime loop), the light's grouped position (-1 = runtime), and whether the rect
 // bounds are the compile-time HEAD scene (CONSTGEO) or read from the uploaded scene (s_load).
-// MAT: SPEC/REFR materials may occur (generic kernel); the specialisations are all-DIFF scenes.
+// MAT: SPEC/REFR materials and the uniform-hemisphere flag may occur (generic kernel); the
+// specialisations are all-DIFF, cosine-scatter scenes (keeps their cosine block branch-free).
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
@@ -273,6 +277,10 @@ constexpr int kRegions = 10;
   } while (0)
 #endif
 
+__device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
+  return (uint32_t)(((uint64_t)n * m) >> sh);
+}
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -383,14 +391,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       if (needs_unit && rank < avail) {
         const uint32_t u = pool_next + rank;
         const uint32_t npix = (uint32_t)Q->n_local_pix, w = (uint32_t)Q->width;
-        const uint32_t j = u / npix;  // chunk-major: lanes get adjacent pixels
+        const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major: adjacent pixels
         lp = u - j * npix;
         s = j * (uint32_t)Q->chunk;
         s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
-        const uint32_t lr = lp / w;
+        const uint32_t lr = div_magic(lp, Q->m_w, Q->sh_w);
         px = (int)(lp - lr * w);
         const uint32_t T_ = (uint32_t)Q->tile_rows;
-        const uint32_t tile = lr / T_, within = lr - tile * T_;
+        const uint32_t tile = div_magic(lr, Q->m_tile, Q->sh_tile), within = lr - tile * T_;
         py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
         pix = (uint32_t)py * w + (uint32_t)px;
         has_unit = true;
@@ -414,9 +422,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       f3 v = mk(0, 0, 0);
       if (cont && !(TP::MAT && spec)) {
         SPT_REGION(8);
-        v = cosine_vec<!TP::SPH>(nl, r.z, r.w, cptr(Pg)->scatter_uniform != 0);
+        v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
         if (SPT_PROBE & 8) {
-          const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, cptr(Pg)->scatter_uniform != 0);
+          const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
           if (opq(0u) != 0u) v = v2;
         }
       }
@@ -837,6 +845,15 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
 
 static int tile_rows_of(const spt_params* p) { return p->tile_rows > 0 ? p->tile_rows : 8; }
 
+// Multiply-shift reciprocal of d for 31-bit numerators: l = ceil(log2 d), m = floor(2^(31+l)/d) + 1
+// (< 2^32), n / d = (n * m) >> (31 + l) exactly for all n < 2^31 (Granlund & Montgomery 1994).
+static void magic31(uint32_t d, uint32_t* m, uint32_t* sh) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  *m = (uint32_t)(((unsigned __int128)1 << (31 + l)) / d + 1);
+  *sh = 31 + l;
+}
+
 // Does the uploaded scene's grouped geometry equal the compile-time HEAD scene bit for bit?
 static bool cornell_const_match(const SceneGeo& g, int light_pos) {
   if (g.n_xy != kCornellNXY || g.n_xz != kCornellNXZ || g.n_yz != kCornellNYZ || g.n_sph != 0 ||
@@ -985,7 +1002,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
   const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
   if (n_units >= 0xFFFF0000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
+  if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
+  magic31((uint32_t)K.n_local_pix, &K.m_npix, &K.sh_npix);
+  magic31((uint32_t)p->width, &K.m_w, &K.sh_w);
+  magic31((uint32_t)K.tile_rows, &K.m_tile, &K.sh_tile);
   K.inv_spp = 1.0f / (float)p->spp;
   K.inv_w = 1.0f / (float)p->width;
   K.inv_h = 1.0f / (float)p->height;
@@ -1014,10 +1035,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const SceneGeo& g = *c->h_geo;
   bool all_diff = true;
   for (int i = 0; i < n_prims; ++i) all_diff = all_diff && prims[i].refl == SPT_DIFF;
-  const bool cornell = all_diff && g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 &&
-                       light_pos == 8;
-  static const bool no_const = std::getenv("SPT_NO_CONST_SCENE") != nullptr;  // A/B switch
-  const bool cconst = !no_const && cornell_const_match(g, light_pos);
+  // The HEAD-topology kernels are all-DIFF, cosine-scatter specialisations; anything else (SPEC/
+  // REFR, the uniform hemisphere) runs the generic kernel.
+  // SPT_KERNEL=generic|cornell (A/B and tests): cap the specialisation level.
+  const char* kenv = std::getenv("SPT_KERNEL");
+  const int kcap = !kenv ? 2 : std::strcmp(kenv, "generic") == 0 ? 0 : std::strcmp(kenv, "cornell") == 0 ? 1 : 2;
+  const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
+                       g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
+  const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
   const int grid = c->n_cu * (cconst    ? c->blocks_per_cu_const
                               : cornell ? c->blocks_per_cu_cornell
                                         : c->blocks_per_cu);

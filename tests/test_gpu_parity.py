@@ -84,6 +84,29 @@ def test_specular_refractive_scene_bit_exact(spt, oracle, case):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+@pytest.mark.parametrize("kernel", ["generic", "cornell"])
+@pytest.mark.parametrize("est,q,fl", [("nee", 1.0, 0), ("cos", 0.0, 0)])
+def test_every_kernel_specialisation_bit_exact(spt, oracle, monkeypatch, kernel, est, q, fl):
+    """The HEAD scene through the generic kernel and the runtime-geometry Cornell kernel too
+    (the default run takes the compile-time-geometry kernel): same contract, same bits."""
+    monkeypatch.setenv("SPT_KERNEL", kernel)
+    p = spt.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
+    _assert_exact(gpu, cpu)
+    assert hashlib.md5(gpu.tobytes()).hexdigest() == GOLD["counter_md5"][est]
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
+def test_specialisation_needs_all_diff(spt, oracle):
+    """A HEAD-geometry scene with one SPEC rectangle must leave the all-DIFF specialisations."""
+    prims = spt.cornell_scene()
+    prims[12].refl = spt.SPEC  # short box front face becomes a mirror
+    p = spt.default_params(width=40, height=30, spp=6, seed=15)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
 def test_chunk_size_never_changes_results(spt):
     cam = spt.Camera(aspect=40 / 30)
     imgs = [spt.render(spt.cornell_scene(), cam, spt.default_params(width=40, height=30, spp=24, chunk=c))
