@@ -237,6 +237,16 @@ def main() -> None:
             traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+    if os.path.exists(pmc_path) and args.config == "c3":
+        try:
+            der = json.load(open(pmc_path))["derived"]
+            pmc = {"valu_issue_frac": round(der["valu_issue_frac_of_peak"], 3),
+                   "valu_lane_utilization": round(der["valu_lane_utilization"], 3),
+                   "source": "profiles/r01_pmc_summary.json (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU)"}
+        except Exception:  # noqa: BLE001
+            pmc = {}
 
     if rank == 0:
         img = full.cpu().numpy()
@@ -266,6 +276,8 @@ def main() -> None:
                                      if traffic else None),
                          "hbm_frac": (round(traffic / (kms.mean() * 1e-3) / 8e12, 5)
                                       if traffic else None),
+                         "frac_vs_nonpacked_78p6": round(achieved / (PEAK_FP32_TFLOPS / 2), 4),
+                         "valu_pmc": pmc or None,
                          "kernel": "spt::render_kernel",
                          "kernel_ms": round(float(kms.mean()), 3),
                          "flop_per_launch": float(flop.mean()),
