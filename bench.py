@@ -77,6 +77,38 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
             "gpu_rows_bit_exact": bool(exact)}
 
 
+def reference_baseline(cfg, budget_s: float):
+    """The reference itself (oracle/_ref/smallpt_{nee,cos}: /root/reference/src/smallpt.cpp compiled
+    by oracle/build_ref.sh with the SURVEY Appendix A patch; single-threaded, as the reference's
+    OpenMP pragma :526 is commented out) on the same image size, with spp scaled to a bounded
+    sample of ~budget_s; None when the binary is absent (it is built only where the reference is)."""
+    import subprocess
+    import tempfile
+
+    if cfg["scene"] != "cornell" or cfg["max_depth"] != 0:
+        return None
+    binary = os.path.join(ROOT, "oracle", "_ref", "smallpt_nee" if cfg["nee_prob"] >= 1 else "smallpt_cos")
+    if not os.path.exists(binary):
+        return None
+    w, h = cfg["width"], cfg["height"]
+    with tempfile.TemporaryDirectory() as tmp:
+        def run(spp):
+            t0 = time.perf_counter()
+            subprocess.run([binary, str(w), str(h), str(spp), "1", os.path.join(tmp, "o.ppm")],
+                           check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            return time.perf_counter() - t0
+        spp = 1
+        dt = run(spp)
+        if dt < budget_s / 2:
+            spp = max(2, int(budget_s / 2 / dt + 0.5))
+            dt = run(spp)
+    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1,
+            "kind": "reference",
+            "sample": f"{w}x{h} @ {spp} spp = {w * h * spp} samples in {dt:.1f} s (whole image incl. "
+                      f"its P3 write); {os.path.relpath(binary, ROOT)} = the reference compiled from "
+                      f"its own sources, g++ -O3, single thread as shipped"}
+
+
 def image_writer(spt, full, w, h, with_cpu: bool):
     """§8(f) output formats: the GPU encoder (spt_image.hip) on the resident framebuffer, P3 as the
     reference writes it (:548-551) and P6/PFM; HBM bytes = 12 B/pixel read + encoded bytes written
@@ -251,8 +283,14 @@ def main() -> None:
     if rank == 0:
         img = full.cpu().numpy()
         cpu = None
+        port = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
+            cpu = reference_baseline(cfg, args.cpu_budget)
+            port = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
+            if cpu is None:
+                cpu = port
+            else:
+                cpu["port"] = port
         if args.save_ppm:
             spt.write_ppm(args.save_ppm, img)
         writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)

@@ -332,8 +332,9 @@ int spt_oracle_write_ppm_f(const char* path, int w, int h, const float* c) {
 }
 
 /* The same files in memory (test checker for the GPU encoder, spt_image.hip): format 0 = P3 exactly
-   as :549-551, 1 = P6 (bytes of toInt), 2 = PFM (little-endian floats, bottom-to-top scanlines,
-   scale text "-1.0" padded with zeros so the data starts dword-aligned). Returns the length, or
+   as :549-551, 1 = P6 (bytes of toInt; header padded with spaces to 16 bytes), 2 = PFM
+   (little-endian floats, bottom-to-top scanlines, scale "-1.0" padded with zeros so the data
+   starts 16-byte aligned). Returns the length, or
    the needed length if cap is too small (nothing written then). */
 size_t spt_oracle_encode_image(const float* c, int w, int h, int format, unsigned char* out,
                                size_t cap) {
@@ -358,7 +359,10 @@ size_t spt_oracle_encode_image(const float* c, int w, int h, int format, unsigne
     return n;
   }
   if (format == 1) {
-    n = (size_t)snprintf(hd, sizeof hd, "P6\n%d %d\n255\n", w, h);
+    n = (size_t)snprintf(hd, sizeof hd, "P6\n%d %d", w, h);
+    while ((n + 5) % 16) hd[n++] = ' ';  /* header padded to 16 bytes (legal PPM whitespace) */
+    memcpy(hd + n, "\n255\n", 5);
+    n += 5;
     if (n + 3 * np > cap) return n + 3 * np;
     memcpy(out, hd, n);
     for (i = 0; i < 3 * np; i++) out[n + i] = (unsigned char)o_toInt(c[i]);
@@ -367,7 +371,7 @@ size_t spt_oracle_encode_image(const float* c, int w, int h, int format, unsigne
   {
     int y;
     n = (size_t)snprintf(hd, sizeof hd, "PF\n%d %d\n-1.0", w, h);
-    while ((n + 1) % 4) hd[n++] = '0';
+    while ((n + 1) % 16) hd[n++] = '0';
     hd[n++] = '\n';
     if (n + 12 * np > cap) return n + 12 * np;
     memcpy(out, hd, n);

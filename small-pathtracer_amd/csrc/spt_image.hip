@@ -14,6 +14,7 @@
 // INT_MIN, as the reference binary does.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -29,7 +30,6 @@ constexpr int kThreads = 256;
 constexpr int kPixPerThread = 4;
 constexpr int kPixPerBlock = kThreads * kPixPerThread;  // 1024
 constexpr int kMaxValueText = 12;                        // "-2147483648 "
-constexpr int kStageBytes = kPixPerBlock * 3 * kMaxValueText + 16;
 
 struct Thresholds { float t[256]; };  // t[k] = smallest x with toInt(x) >= k; t[0] = -inf
 
@@ -55,12 +55,17 @@ static const Thresholds& thresholds() {
   return T;
 }
 
+// toInt(x) = #{k >= 1 : x >= thr[k]}: a hardware estimate pow(x, 1/2.2)*255 + .5 (v_log/v_exp, a
+// few ulps) lands within one step of the exact count; the table then settles it exactly
+// (thresholds are >= ~1e-6 apart in relative terms, the estimate is ~1e-6 accurate).
 __device__ __forceinline__ int dev_toInt(const float* __restrict__ thr, float x) {
   if (x != x) return (int)0x80000000;  // int(NaN) on x86-64 (cvttsd2si)
-  int idx = 0;
-#pragma unroll
-  for (int step = 128; step >= 1; step >>= 1) idx = x >= thr[idx + step] ? idx + step : idx;
-  return idx;
+  const float xc = fminf(fmaxf(x, 0.0f), 1.0f);
+  const float est = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(xc) * (1.0f / 2.2f)) * 255.0f + 0.5f;
+  int v = (int)fminf(fmaxf(est, 0.0f), 255.0f);
+  if (v < 255 && x >= thr[v + 1]) ++v;  // thr[0] = -inf, so x >= thr[v] below always holds at v = 0
+  else if (x < thr[v]) --v;
+  return v;
 }
 
 __device__ __forceinline__ uint32_t text_len(int v) {
@@ -108,74 +113,124 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   return base + incl - v;
 }
 
+// ---- single-pass P3: decoupled look-back (Merrill & Garland 2016) over 1024-pixel blocks.
+// Blocks take a ticket at start, so every predecessor of a block is resident or finished and the
+// look-back always makes progress. status[b] = flag << 62 | value: flag 1 = the block's own
+// aggregate, 2 = its inclusive prefix (header included). Agent-scope atomics on the status words
+// keep the hand-off coherent across the XCDs' L2s.
+constexpr int kStageP3 = kPixPerBlock * 3 * 4 + 16;  // every value of a block <= "255 ": 12 KB
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+// Relaxed agent-scope atomics: the status word is the only datum that crosses blocks (no other
+// memory is read after it), so no acquire/release fences — at agent scope those cost an L1
+// invalidate / an L2 write-back of the block's dirty text per step (MI355X_MICROARCH.md).
+__device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void __launch_bounds__(kThreads)
-p3_lengths(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint32_t* __restrict__ block_len) {
+p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t header_len,
+          uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint8_t* __restrict__ out,
+          uint64_t cap, uint64_t* __restrict__ total_out) {
   __shared__ float s_thr[256];
   __shared__ uint32_t s_wave[kThreads / 64];
-  load_thr(s_thr, T);
-  const uint64_t v0 = ((uint64_t)blockIdx.x * kPixPerBlock + (uint64_t)threadIdx.x * kPixPerThread) * 3;
-  const uint64_t nv = (uint64_t)n_pix * 3;
-  uint32_t len = 0;
+  __shared__ __attribute__((aligned(16))) uint8_t s_txt[kStageP3];
+  __shared__ uint32_t s_bid;
+  __shared__ uint64_t s_prefix;
+  if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
+  load_thr(s_thr, T);  // barrier
+  const uint32_t bid = s_bid;
+  const uint64_t b0 = (uint64_t)bid * kPixPerBlock * 3, nv = (uint64_t)n_pix * 3;
+  const uint64_t v0 = b0 + (uint64_t)threadIdx.x * kPixPerThread * 3;
+  float x[kPixPerThread * 3];
+  if (v0 + kPixPerThread * 3 <= nv) {  // 48 contiguous bytes per thread: three float4 loads
+    const float4* q = (const float4*)(rgb + v0);
 #pragma unroll
-  for (int i = 0; i < kPixPerThread * 3; ++i)
-    if (v0 + i < nv) len += text_len(dev_toInt(s_thr, rgb[v0 + i]));
-  uint32_t total;
-  (void)block_excl_scan(len, s_wave, &total);
-  if (threadIdx.x == 0) block_len[blockIdx.x] = total;
-}
-
-// Exclusive scan of the block lengths (one block of 1024 threads, sequential tiles with a carry).
-__global__ void __launch_bounds__(1024)
-scan_blocks(const uint32_t* __restrict__ block_len, uint64_t* __restrict__ block_off, uint32_t n,
-            uint64_t header, uint64_t* __restrict__ total) {
-  __shared__ uint64_t s[1024];
-  uint64_t carry = header;
-  for (uint32_t base = 0; base < n; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    const uint64_t v = i < n ? block_len[i] : 0;
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-      const uint64_t u = threadIdx.x >= (unsigned)off ? s[threadIdx.x - off] : 0;
-      __syncthreads();
-      s[threadIdx.x] += u;
-      __syncthreads();
+    for (int k = 0; k < 3; ++k) {
+      const float4 f = q[k];
+      x[4 * k] = f.x; x[4 * k + 1] = f.y; x[4 * k + 2] = f.z; x[4 * k + 3] = f.w;
     }
-    if (i < n) block_off[i] = carry + s[threadIdx.x] - v;
-    const uint64_t tile = s[1023];
-    __syncthreads();
-    carry += tile;
+  } else {
+#pragma unroll
+    for (int i = 0; i < kPixPerThread * 3; ++i) x[i] = v0 + i < nv ? rgb[v0 + i] : 0.0f;
   }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-__global__ void __launch_bounds__(kThreads)
-p3_write(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T,
-         const uint64_t* __restrict__ block_off, uint8_t* __restrict__ out) {
-  __shared__ float s_thr[256];
-  __shared__ uint32_t s_wave[kThreads / 64];
-  __shared__ __attribute__((aligned(16))) uint8_t s_txt[kStageBytes];
-  load_thr(s_thr, T);
-  const uint64_t v0 = ((uint64_t)blockIdx.x * kPixPerBlock + (uint64_t)threadIdx.x * kPixPerThread) * 3;
-  const uint64_t nv = (uint64_t)n_pix * 3;
   int vals[kPixPerThread * 3];
   uint32_t len = 0;
 #pragma unroll
   for (int i = 0; i < kPixPerThread * 3; ++i) {
-    vals[i] = v0 + i < nv ? dev_toInt(s_thr, rgb[v0 + i]) : 0;
-    len += v0 + i < nv ? text_len(vals[i]) : 0u;
+    const bool in = v0 + i < nv;
+    vals[i] = in ? dev_toInt(s_thr, x[i]) : 0;
+    len += in ? text_len(vals[i]) : 0u;
   }
   uint32_t total;
   const uint32_t my = block_excl_scan(len, s_wave, &total);
-  const uint64_t dst = block_off[blockIdx.x];
+  if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors per step
+    const uint32_t lane = threadIdx.x;
+    uint64_t excl = header_len;
+    if (bid == 0) {
+      if (lane == 0) status_store(status, kFlagInc | (header_len + total));
+    } else {
+      if (lane == 0) status_store(status + bid, kFlagAgg | total);
+      excl = 0;
+      int64_t top = (int64_t)bid - 1;  // window [top - 63, top], lane l reads top - l
+      uint32_t spins = 0;
+      while (top >= 0) {
+        const int64_t j = top - (int64_t)lane;
+        const uint64_t st = j >= 0 ? status_load(status + j) : kFlagInc;  // "before block 0" = 0
+        const uint32_t flag = (uint32_t)(st >> 62);
+        const uint64_t ready = __ballot(flag != 0), inc = __ballot(flag == 2);
+        const uint32_t n_inc = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive
+        const uint64_t need = n_inc == 64u ? ~0ull : ((2ull << n_inc) - 1);   // lanes 0..n_inc
+        if ((ready & need) != need) {  // a predecessor in the window has not published yet
+          if (++spins > (1u << 24)) {  // cannot happen (tickets order the blocks); never hang
+            if (lane == 0) *total_out = ~0ull;
+            break;
+          }
+          continue;
+        }
+        uint64_t v = lane <= n_inc && j >= 0 ? (st & kValMask) : 0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        excl += v;
+        if (n_inc < 64u) break;
+        top -= 64;
+      }
+      if (lane == 0) status_store(status + bid, kFlagInc | (excl + total));
+    }
+    if (lane == 0) {
+      s_prefix = excl;
+      if (bid == gridDim.x - 1) *total_out = excl + total;
+    }
+  }
+  __syncthreads();
+  const uint64_t dst = s_prefix;
+  if (total + 16 > (uint32_t)kStageP3) {  // NaN-heavy block: direct byte stores, no staging
+    uint64_t q = dst + my;
+#pragma unroll
+    for (int i = 0; i < kPixPerThread * 3; ++i) {
+      if (v0 + i >= nv) break;
+      uint8_t b[12];
+      const uint32_t n = put_value(b, vals[i]);
+      for (uint32_t k = 0; k < n; ++k, ++q)
+        if (q < cap) out[q] = b[k];
+    }
+    return;
+  }
   const uint32_t phase = (uint32_t)(dst & 3u);  // stage at the destination's dword phase
   uint8_t* p = s_txt + phase + my;
 #pragma unroll
   for (int i = 0; i < kPixPerThread * 3; ++i)
     if (v0 + i < nv) p += put_value(p, vals[i]);
   __syncthreads();
-  // bytes [dst, dst + total) <- s_txt[phase, phase + total)
-  const uint64_t a0 = (dst + 3u) & ~3ull, a1 = (dst + total) & ~3ull;  // aligned middle
+  if (dst + total > cap) {  // the host reports the error; write nothing past cap
+    for (uint32_t i = threadIdx.x; i < total; i += kThreads)
+      if (dst + i < cap) out[dst + i] = s_txt[phase + i];
+    return;
+  }
+  const uint64_t a0 = (dst + 3u) & ~3ull, a1 = (dst + total) & ~3ull;
   if (a0 >= a1) {
     for (uint32_t i = threadIdx.x; i < total; i += kThreads) out[dst + i] = s_txt[phase + i];
     return;
@@ -184,41 +239,75 @@ p3_write(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T,
   if (threadIdx.x < head) out[dst + threadIdx.x] = s_txt[phase + threadIdx.x];
   if (threadIdx.x < tail) out[a1 + threadIdx.x] = s_txt[phase + (uint32_t)(a1 - dst) + threadIdx.x];
   const uint32_t n_dw = (uint32_t)((a1 - a0) >> 2);
-  const uint32_t* s_dw = (const uint32_t*)(s_txt + phase + head);  // dword-aligned in LDS
+  const uint32_t* s_dw = (const uint32_t*)(s_txt + phase + head);
   uint32_t* o_dw = (uint32_t*)(out + a0);
   for (uint32_t i = threadIdx.x; i < n_dw; i += kThreads) o_dw[i] = s_dw[i];
 }
 
-// P6: header, then toInt bytes (unsigned char of the int, as a byte-writing port would store).
+// P6: header (padded to 16 bytes, see header()), then toInt bytes (the int's low byte, as a
+// byte-writing port would store). Grid-stride over float4 chunks: 4 values -> one dword store.
 __global__ void __launch_bounds__(kThreads)
-p6_write(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint8_t* __restrict__ out) {
+p6_write(const float4* __restrict__ rgb, uint32_t n_vals, Thresholds T, uint32_t* __restrict__ out) {
   __shared__ float s_thr[256];
   load_thr(s_thr, T);
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i < (uint64_t)n_pix * 3) out[i] = (uint8_t)dev_toInt(s_thr, rgb[i]);
+  const uint32_t n4 = n_vals / 4;
+  for (uint32_t c = blockIdx.x * kThreads + threadIdx.x; c < n4; c += gridDim.x * kThreads) {
+    const float4 v = rgb[c];
+    out[c] = (uint32_t)(uint8_t)dev_toInt(s_thr, v.x) | (uint32_t)(uint8_t)dev_toInt(s_thr, v.y) << 8 |
+             (uint32_t)(uint8_t)dev_toInt(s_thr, v.z) << 16 | (uint32_t)(uint8_t)dev_toInt(s_thr, v.w) << 24;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n_vals & 3u)) {  // ragged tail (n_vals % 4 values)
+    const uint32_t i = n4 * 4 + threadIdx.x;
+    ((uint8_t*)out)[i] = (uint8_t)dev_toInt(s_thr, ((const float*)rgb)[i]);
+  }
 }
 
-// PFM: little-endian float RGB, scanlines bottom to top; the header is padded to a dword multiple
-// so every float store is aligned.
+// PFM: little-endian float RGB, scanlines bottom to top. Rows of 3w floats; when w % 4 == 0 a row
+// is whole float4 chunks and the (16-byte padded) header keeps every store 16-byte aligned.
 __global__ void __launch_bounds__(kThreads)
-pfm_write(const float* __restrict__ rgb, uint32_t w, uint32_t h, uint32_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  const uint64_t row_f = (uint64_t)w * 3;
-  if (i >= row_f * h) return;
-  const uint64_t y = i / row_f, r = i - y * row_f;
-  out[(h - 1 - y) * row_f + r] = __float_as_uint(rgb[i]);
+pfm_write4(const float4* __restrict__ rgb, uint32_t row4, uint32_t h, uint32_t m_row, uint32_t sh_row,
+           float4* __restrict__ out) {
+  const uint32_t n4 = row4 * h;
+  for (uint32_t c = blockIdx.x * kThreads + threadIdx.x; c < n4; c += gridDim.x * kThreads) {
+    const uint32_t y = (uint32_t)(((uint64_t)c * m_row) >> sh_row), r = c - y * row4;
+    out[(h - 1 - y) * row4 + r] = rgb[c];
+  }
+}
+__global__ void __launch_bounds__(kThreads)
+pfm_write1(const float* __restrict__ rgb, uint32_t row, uint32_t h, uint32_t m_row, uint32_t sh_row,
+           float* __restrict__ out) {
+  const uint32_t n = row * h;
+  for (uint32_t c = blockIdx.x * kThreads + threadIdx.x; c < n; c += gridDim.x * kThreads) {
+    const uint32_t y = (uint32_t)(((uint64_t)c * m_row) >> sh_row), r = c - y * row;
+    out[(h - 1 - y) * row + r] = rgb[c];
+  }
 }
 
+// n / d = (n * m) >> sh for n < 2^31 (same construction as the render kernel's refill)
+static void magic31(uint32_t d, uint32_t* m, uint32_t* sh) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  *m = (uint32_t)(((unsigned __int128)1 << (31 + l)) / d + 1);
+  *sh = 31 + l;
+}
+
+// P3 is the reference's header exactly. P6 and PFM pad their header to a multiple of 16 bytes so
+// the raster starts 16-byte aligned: P6 with spaces before the final newline of the size line
+// (any whitespace may separate tokens in a PPM header), PFM with zeros in the scale ("-1.000...").
 static std::string header(int w, int h, int format) {
   char b[96];
-  if (format == SPT_IMAGE_P3) std::snprintf(b, sizeof b, "P3\n%d %d\n%d\n", w, h, 255);  // :549
-  else if (format == SPT_IMAGE_P6) std::snprintf(b, sizeof b, "P6\n%d %d\n255\n", w, h);
-  else {
-    std::string s = "PF\n" + std::to_string(w) + " " + std::to_string(h) + "\n-1.0";
-    while ((s.size() + 1) % 4) s += "0";  // "-1.0", "-1.00", ... : data starts dword-aligned
-    return s + "\n";
+  if (format == SPT_IMAGE_P3) {
+    std::snprintf(b, sizeof b, "P3\n%d %d\n%d\n", w, h, 255);  // :549
+    return b;
   }
-  return b;
+  if (format == SPT_IMAGE_P6) {
+    std::string s = "P6\n" + std::to_string(w) + " " + std::to_string(h);
+    while ((s.size() + 5) % 16) s += " ";
+    return s + "\n255\n";
+  }
+  std::string s = "PF\n" + std::to_string(w) + " " + std::to_string(h) + "\n-1.0";
+  while ((s.size() + 1) % 16) s += "0";
+  return s + "\n";
 }
 
 }  // namespace spt_img
@@ -227,8 +316,7 @@ using namespace spt_img;
 
 struct spt_encoder {
   int device = 0;
-  uint32_t* block_len = nullptr;
-  uint64_t* block_off = nullptr;
+  uint64_t* status = nullptr;    // single-pass P3 look-back words + ticket
   uint32_t cap_blocks = 0;
   uint64_t* total = nullptr;     // device word: encoded length
   uint64_t* h_total = nullptr;   // pinned mirror
@@ -277,8 +365,7 @@ extern "C" spt_status spt_encoder_create(int32_t device, spt_encoder** out) {
 extern "C" spt_status spt_encoder_destroy(spt_encoder* e) {
   if (!e) return SPT_OK;
   (void)hipSetDevice(e->device);
-  if (e->block_len) (void)hipFree(e->block_len);
-  if (e->block_off) (void)hipFree(e->block_off);
+  if (e->status) (void)hipFree(e->status);
   if (e->total) (void)hipFree(e->total);
   if (e->h_total) (void)hipHostFree(e->h_total);
   delete e;
@@ -300,42 +387,47 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
   uint64_t len;
   if (format == SPT_IMAGE_P3) {
     const uint32_t nb = (n_pix + kPixPerBlock - 1) / kPixPerBlock;
-    if (nb > e->cap_blocks) {
-      if (e->block_len) IMG_HIP(hipFree(e->block_len));
-      if (e->block_off) IMG_HIP(hipFree(e->block_off));
-      e->block_len = nullptr;
-      e->block_off = nullptr;
+    if (nb + 1 > e->cap_blocks) {  // status words [0, nb) + the ticket
+      if (e->status) IMG_HIP(hipFree(e->status));
+      e->status = nullptr;
       e->cap_blocks = 0;
-      IMG_HIP(hipMalloc(&e->block_len, sizeof(uint32_t) * nb));
-      IMG_HIP(hipMalloc(&e->block_off, sizeof(uint64_t) * nb));
-      e->cap_blocks = nb;
+      IMG_HIP(hipMalloc(&e->status, sizeof(uint64_t) * (nb + 1)));
+      e->cap_blocks = nb + 1;
     }
-    hipLaunchKernelGGL(p3_lengths, dim3(nb), dim3(kThreads), 0, stream, rgb_dev, n_pix, T, e->block_len);
-    IMG_HIP(hipGetLastError());
-    hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, stream, (const uint32_t*)e->block_len,
-                       e->block_off, nb, (uint64_t)hd.size(), e->total);
+    IMG_HIP(hipMemsetAsync(e->status, 0, sizeof(uint64_t) * (nb + 1), stream));
+    if (cap >= hd.size()) IMG_HIP(hipMemcpyAsync(out_dev, hd.data(), hd.size(), hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(p3_single, dim3(nb), dim3(kThreads), 0, stream, rgb_dev, n_pix, T,
+                       (uint64_t)hd.size(), (uint32_t*)(e->status + nb), e->status, out_dev, cap, e->total);
     IMG_HIP(hipGetLastError());
     IMG_HIP(hipMemcpyAsync(e->h_total, e->total, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
     IMG_HIP(hipStreamSynchronize(stream));  // the text length is data-dependent
     len = *e->h_total;
     *len_out = len;
     if (len > cap) return img_fail(SPT_ERR_INVALID_ARG, "output buffer too small (need " + std::to_string(len) + " bytes)");
-    IMG_HIP(hipMemcpyAsync(out_dev, hd.data(), hd.size(), hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(p3_write, dim3(nb), dim3(kThreads), 0, stream, rgb_dev, n_pix, T,
-                       (const uint64_t*)e->block_off, out_dev);
-    IMG_HIP(hipGetLastError());
   } else {
     len = hd.size() + (uint64_t)n_pix * (format == SPT_IMAGE_P6 ? 3 : 12);
     *len_out = len;
     if (len > cap) return img_fail(SPT_ERR_INVALID_ARG, "output buffer too small (need " + std::to_string(len) + " bytes)");
     IMG_HIP(hipMemcpyAsync(out_dev, hd.data(), hd.size(), hipMemcpyHostToDevice, stream));
-    const uint64_t nv = (uint64_t)n_pix * 3;
-    const dim3 grid((unsigned)((nv + kThreads - 1) / kThreads));
-    if (format == SPT_IMAGE_P6)
-      hipLaunchKernelGGL(p6_write, grid, dim3(kThreads), 0, stream, rgb_dev, n_pix, T, out_dev + hd.size());
-    else
-      hipLaunchKernelGGL(pfm_write, grid, dim3(kThreads), 0, stream, rgb_dev, (uint32_t)w, (uint32_t)h,
+    const uint32_t nv = n_pix * 3;
+    // grid-stride loops over ~8 blocks per CU (the block prologue stages the toInt table)
+    const uint32_t grid = std::max(1u, std::min((nv / 4 + kThreads - 1) / kThreads, 2048u));
+    if (((uintptr_t)rgb_dev & 15u) || ((uintptr_t)(out_dev + hd.size()) & 15u))
+      return img_fail(SPT_ERR_INVALID_ARG, "framebuffer and output must be 16-byte aligned");
+    if (format == SPT_IMAGE_P6) {
+      hipLaunchKernelGGL(p6_write, dim3(grid), dim3(kThreads), 0, stream, (const float4*)rgb_dev, nv, T,
                          (uint32_t*)(out_dev + hd.size()));
+    } else if (w % 4 == 0) {
+      uint32_t m, sh;
+      magic31((uint32_t)w * 3 / 4, &m, &sh);
+      hipLaunchKernelGGL(pfm_write4, dim3(grid), dim3(kThreads), 0, stream, (const float4*)rgb_dev,
+                         (uint32_t)w * 3 / 4, (uint32_t)h, m, sh, (float4*)(out_dev + hd.size()));
+    } else {
+      uint32_t m, sh;
+      magic31((uint32_t)w * 3, &m, &sh);
+      hipLaunchKernelGGL(pfm_write1, dim3(grid * 4), dim3(kThreads), 0, stream, rgb_dev, (uint32_t)w * 3,
+                         (uint32_t)h, m, sh, (float*)(out_dev + hd.size()));
+    }
     IMG_HIP(hipGetLastError());
   }
   return SPT_OK;

@@ -118,10 +118,12 @@ def test_oracle_p6_pfm_layout(oracle):
     p3 = oracle.encode_image(rgb, 0)
     p6 = oracle.encode_image(rgb, 1)
     vals = [int(v) for v in p3.split(b"\n", 3)[3].split()]
-    assert p6.startswith(b"P6\n7 5\n255\n") and list(p6[len(b"P6\n7 5\n255\n"):]) == vals
+    hd6 = p6[: p6.index(b"255\n") + 4]  # "P6\n7 5<spaces>\n255\n", padded to 16 bytes
+    assert hd6.split() == [b"P6", b"7", b"5", b"255"] and len(hd6) % 16 == 0
+    assert list(p6[len(hd6):]) == vals
     pfm = oracle.encode_image(rgb, 2)
     hd = pfm[: pfm.index(b"\n", pfm.index(b"\n", 3) + 1) + 1]
-    assert hd.startswith(b"PF\n7 5\n-1.0") and len(hd) % 4 == 0 and float(hd.split()[3]) == -1.0
+    assert hd.startswith(b"PF\n7 5\n-1.0") and len(hd) % 16 == 0 and float(hd.split()[3]) == -1.0
     data = np.frombuffer(pfm[len(hd):], dtype="<f4").reshape(5, 7, 3)
     assert np.array_equal(data[::-1], rgb) and struct.calcsize("<f") == 4
 
