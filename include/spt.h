@@ -144,8 +144,9 @@ typedef struct spt_context spt_context;
 spt_status spt_context_create(int32_t device, spt_context** out);
 spt_status spt_context_destroy(spt_context* ctx);
 /* Enqueue a render on `stream` (a hipStream_t, NULL = default stream). rgb_dev: DEVICE buffer of
- * shard_rows*w*3 floats. No host synchronisation, no allocation once the context is large enough
- * (spt_context_reserve), so it may be captured into a hipGraph. */
+ * shard_rows*w*3 floats. No allocation once the context is large enough (spt_context_reserve) and
+ * no host synchronisation, except that a second call before spt_context_stats() first waits for
+ * the previous call's scene upload (the pinned staging buffers are reused). */
 spt_status spt_context_reserve(spt_context* ctx, int32_t n_prims, const spt_params* p);
 spt_status spt_render_async(spt_context* ctx, const spt_prim* prims, int32_t n_prims,
                             const spt_camera* cam, const spt_params* p, float* rgb_dev,
