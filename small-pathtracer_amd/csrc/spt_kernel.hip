@@ -986,6 +986,15 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.ldzi = p->light_mode == SPT_LIGHT_GLIBC_WRAP ? (uint32_t)p->light_dz : 0u;
   K.tile_rows = tile_rows_of(p); K.shard_index = p->shard_index; K.shard_count = p->shard_count;
   const int rows = spt_shard_row_count(p);
+  if (rows == 0) {  // a shard that owns no rows (more shards than row tiles): nothing to render
+    c->samples = 0;
+    c->scene_flop = 0;
+    SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
+    SPT_HIP(hipEventRecord(c->ev0, stream));
+    SPT_HIP(hipEventRecord(c->ev1, stream));
+    c->pending = true;
+    return SPT_OK;
+  }
   K.n_local_pix = rows * p->width;
   // Unit size: ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured
   // 25.0 ms vs 26.0 ms at 8 units/lane and 27.8 ms at 2); never changes results (integer
@@ -1116,6 +1125,11 @@ extern "C" spt_status spt_render(const spt_prim* prims, int32_t n_prims, const s
   st = spt_context_create(p->device, &c);
   if (st != SPT_OK) return st;
   const size_t n = 3ull * (size_t)spt_shard_row_count(p) * (size_t)p->width;
+  if (n == 0) {  // this shard owns no rows
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    spt_context_destroy(c);
+    return SPT_OK;
+  }
   float* dev = nullptr;
   hipError_t e = hipMalloc(&dev, n * sizeof(float));
   if (e != hipSuccess) {

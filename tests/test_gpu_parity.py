@@ -107,6 +107,29 @@ def test_specialisation_needs_all_diff(spt, oracle):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+def test_more_shards_than_row_tiles(spt):
+    """height 5 in 4-row tiles over 8 shards: shards 2..7 own no rows and return an empty result."""
+    cam = spt.Camera(aspect=16 / 5)
+    full = spt.render(spt.cornell_scene(), cam, spt.default_params(width=16, height=5, spp=4))
+    out = np.zeros_like(full)
+    for k in range(8):
+        p = spt.default_params(width=16, height=5, spp=4, shard_index=k, shard_count=8, tile_rows=4)
+        img, st = spt.render(spt.cornell_scene(), cam, p, return_stats=True)
+        rows = spt.shard_rows(p)
+        assert img.shape[0] == len(rows) and st["samples"] == len(rows) * 16 * 4
+        if len(rows):
+            out[rows] = img
+    assert np.array_equal(out, full)
+
+
+def test_high_spp_tiny_image(spt, oracle):
+    """65536 spp on 4x3 pixels: 64-bit fixed-point sums and many units per pixel."""
+    p = spt.default_params(width=4, height=3, spp=65536, seed=21)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
 def test_chunk_size_never_changes_results(spt):
     cam = spt.Camera(aspect=40 / 30)
     imgs = [spt.render(spt.cornell_scene(), cam, spt.default_params(width=40, height=30, spp=24, chunk=c))
