@@ -3,15 +3,15 @@
 //
 // The reference writes `fprintf(f, "%d %d %d ", toInt(r), toInt(g), toInt(b))` per pixel: ASCII
 // P3, 6-12 bytes per pixel, ~200 MB of text at 4096². Here the framebuffer never leaves HBM until
-// the bytes are final: three HBM-bound byte passes over the fp32 framebuffer.
-//   pass 1  per-block text length (4 pixels per thread, 1024 per block)
-//   scan    exclusive scan of the block lengths (one block), + header length -> block offsets
-//   pass 3  per-thread text into an LDS staging buffer placed at the destination's dword phase,
-//           then aligned dword stores of the block's contiguous byte range (head/tail bytes apart)
-// toInt is evaluated exactly as the reference's double-precision pow() by a 256-entry threshold
-// table computed on the host with that very formula (toInt is monotone in x): the device counts
-// the thresholds <= x with an 8-step binary search in LDS. NaN prints as x86-64's int(NaN),
-// INT_MIN, as the reference binary does.
+// the bytes are final, in ONE HBM-bound pass (p3_single): each 2048-pixel block loads its values
+// with float4 loads, formats 8 pixels per thread, finds its byte offset by a block scan plus a
+// decoupled look-back over its predecessors' published lengths, stages its text in LDS at the
+// destination's dword phase and writes it with aligned dword stores (head/tail bytes apart).
+// P6 / PFM are fixed-size: grid-stride float4 loops, one dword / float4 store per 4 values.
+// toInt is the reference's double-precision formula exactly: a 256-entry threshold table computed
+// on the host with that very formula (toInt is monotone in x) settles a v_log/v_exp estimate,
+// which is never more than one step off. NaN prints as x86-64's int(NaN), INT_MIN, as the
+// reference binary does.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,8 +27,12 @@
 namespace spt_img {
 
 constexpr int kThreads = 256;
-constexpr int kPixPerThread = 4;
-constexpr int kPixPerBlock = kThreads * kPixPerThread;  // 1024
+#ifndef SPT_P3_PIX_PER_THREAD
+#define SPT_P3_PIX_PER_THREAD 8
+#endif
+constexpr int kPixPerThread = SPT_P3_PIX_PER_THREAD;    // P3: pixels formatted per thread
+constexpr int kPixPerBlock = kThreads * kPixPerThread;  // 2048 (4096² P3: 177 µs at 8, 227 at 4, 193 at 12)
+static_assert(kPixPerThread % 4 == 0, "whole float4 loads per thread");
 constexpr int kMaxValueText = 12;                        // "-2147483648 "
 
 struct Thresholds { float t[256]; };  // t[k] = smallest x with toInt(x) >= k; t[0] = -inf
@@ -113,7 +117,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   return base + incl - v;
 }
 
-// ---- single-pass P3: decoupled look-back (Merrill & Garland 2016) over 1024-pixel blocks.
+// ---- single-pass P3: decoupled look-back (Merrill & Garland 2016) over kPixPerBlock-pixel blocks.
 // Blocks take a ticket at start, so every predecessor of a block is resident or finished and the
 // look-back always makes progress. status[b] = flag << 62 | value: flag 1 = the block's own
 // aggregate, 2 = its inclusive prefix (header included). Agent-scope atomics on the status words
@@ -146,10 +150,10 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   const uint64_t b0 = (uint64_t)bid * kPixPerBlock * 3, nv = (uint64_t)n_pix * 3;
   const uint64_t v0 = b0 + (uint64_t)threadIdx.x * kPixPerThread * 3;
   float x[kPixPerThread * 3];
-  if (v0 + kPixPerThread * 3 <= nv) {  // 48 contiguous bytes per thread: three float4 loads
+  if (v0 + kPixPerThread * 3 <= nv) {  // 12 B per pixel, contiguous per thread: float4 loads
     const float4* q = (const float4*)(rgb + v0);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kPixPerThread * 3 / 4; ++k) {
       const float4 f = q[k];
       x[4 * k] = f.x; x[4 * k + 1] = f.y; x[4 * k + 2] = f.z; x[4 * k + 3] = f.w;
     }
