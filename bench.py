@@ -271,7 +271,7 @@ def main() -> None:
             traffic = None
     pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-    if os.path.exists(pmc_path) and args.config == "c3":
+    if os.path.exists(pmc_path) and args.config == "c3" and world == 1:
         try:
             der = json.load(open(pmc_path))["derived"]
             pmc = {"valu_issue_frac": round(der["valu_issue_frac_of_peak"], 3),
@@ -305,7 +305,8 @@ def main() -> None:
                                                    if scaling == "weak" and world > 1 else ""),
                        "width": w, "height": h, "spp": spp,
                        "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",
-                       "parallelism": f"row-tile x{world} (tile 8 rows, cyclic) + RCCL gather"
+                       "parallelism": (f"row-tile x{world} (tile 8 rows, cyclic) + one gather to rank 0 "
+                                       f"({'RCCL' if backend == 'nccl' else backend})")
                                       if world > 1 else "1 GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
