@@ -41,4 +41,10 @@ build smallpt_cos -e '464s/if (q < 1)/if (q < 0)/'
 # uniform-hemisphere variant of random_scattering: the live cosine body :340-347 removed and the
 # commented-out uniform body :352-359 enabled (its /* and */ lines :351, :360 removed)
 build smallpt_uni -e '340,347d' -e '351d' -e '360d'
-echo "built $OUT/smallpt_nee $OUT/smallpt_cos $OUT/smallpt_uni"
+# statistics-only variant (tests/test_fidelity.py): the per-row erand48 state {0,0,y^3} of :530
+# does not depend on the seed, so every scattering/RR draw repeats across seeds and only rand()
+# (jitter, light point, Q) varies. Seeding the middle word with the seed gives independent runs.
+xs='530s/Xi\[3\] = { 0, 0, y \* y \* y }/Xi[3] = { 0, (unsigned short)seed_, (unsigned short)(y * y * y) }/'
+build smallpt_nee_xs -e "$xs"
+build smallpt_cos_xs -e '464s/if (q < 1)/if (q < 0)/' -e "$xs"
+echo "built $OUT/smallpt_{nee,cos,uni} $OUT/smallpt_{nee,cos}_xs"

@@ -79,14 +79,30 @@ def camera(aspect: float):
 
 
 def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, prims=None,
-                  uniform: bool = False):
-    """fp64 restatement of the reference (bit-exact with the patched oracle). (h, w, 3) float64."""
+                  uniform: bool = False, row_seed: bool = False, stats: bool = False):
+    """fp64 restatement of the reference (bit-exact with the patched oracle). (h, w, 3) float64.
+
+    row_seed: seed erand48's row streams with the seed too (oracle/_ref/smallpt_cos_xs); without it
+    the reference's scattering/RR draws are the same for every seed. stats: also return
+    {"vertices", "misses"} over all radiance() calls."""
     prims = prims or scene_cornell()
     arr = (_spt.spt_prim * len(prims))(*prims)
     out = np.zeros((h, w, 3), dtype=np.float64)
-    lib().spt_oracle_compat_render(arr, len(prims), w, h, spp, seed, int(nee) | (2 if uniform else 0),
-                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    st = (ctypes.c_uint64 * 2)()
+    flags = int(nee) | (2 if uniform else 0) | (4 if row_seed else 0)
+    lib().spt_oracle_compat_render_stats(arr, len(prims), w, h, spp, seed, flags,
+                                         out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), st)
+    if stats:
+        return out, {"vertices": int(st[0]), "misses": int(st[1])}
     return out
+
+
+def plane_k(k: float) -> float:
+    """The contract's fp32 plane coordinate of a rectangle at k (spt_oracle_plane_k)."""
+    L = lib()
+    L.spt_oracle_plane_k.restype = ctypes.c_float
+    L.spt_oracle_plane_k.argtypes = [ctypes.c_double]
+    return float(np.float32(L.spt_oracle_plane_k(k)))
 
 
 def counter_render(prims, cam, params, rows=None, threads: int = 0):

@@ -132,6 +132,7 @@ typedef struct {
   int nee;     /* 1: `q < 1` (HEAD :464), 0: `q < 0` (cosine-only) */
   int uniform; /* random_scattering: 0 = cosine code :340-347, 1 = uniform code :352-359 */
   o_glibc_rand* g;
+  uint64_t vertices, misses; /* radiance() calls and their misses (fidelity statistics) */
 } o_scene;
 
 /* intersect :323-335: strict `<` keeps the lowest index on ties; id untouched on a miss. */
@@ -197,7 +198,8 @@ static dv o_radiance(const o_scene* S, dv ro, dv rd, int depth, unsigned short* 
   int id = 0;
   double t;
   dv x;
-  if (!o_intersect(S, ro, rd, &t, &id)) x = dv3(0, 0, 0); /* hittingPoint :371-377 */
+  ((o_scene*)S)->vertices++;
+  if (!o_intersect(S, ro, rd, &t, &id)) { x = dv3(0, 0, 0); ((o_scene*)S)->misses++; } /* :371-377 */
   else x = dadd(ro, dmul(rd, t));
   {
     const o_prim* obj = &S->prims[id];
@@ -266,10 +268,14 @@ void spt_oracle_camera(double out[12], const double lf[3], const double la[3], c
 }
 
 /* main() :502-542 with the HEAD scene, srand(seed) and the state-space build skipped.
- * nee: bit 0 = `q < 1` (HEAD) vs `q < 0`; bit 1 = uniform random_scattering (:352-359).
- * c_out: w*h*3 doubles (clamped, row-major, y=0 top). Returns 0. */
-int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp, unsigned seed,
-                             int nee, double* c_out) {
+ * nee: bit 0 = `q < 1` (HEAD) vs `q < 0`; bit 1 = uniform random_scattering (:352-359);
+ * bit 2 = row streams {0, seed, y^3} instead of :530's {0, 0, y^3} (oracle/build_ref.sh
+ * smallpt_cos_xs): without it every seed repeats the same scattering/RR draws and only rand()
+ * varies, so seed-to-seed differences understate the estimator's noise.
+ * c_out: w*h*3 doubles (clamped, row-major, y=0 top). stats (may be NULL): {vertices, misses}
+ * over all radiance() calls. Returns 0. */
+int spt_oracle_compat_render_stats(const spt_prim* prims, int n, int w, int h, int spp,
+                                   unsigned seed, int nee, double* c_out, uint64_t* stats) {
   o_prim* P = (o_prim*)malloc(sizeof(o_prim) * (size_t)n);
   o_glibc_rand g;
   o_scene S;
@@ -279,6 +285,7 @@ int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp
   dv origin, llc, hor, ver;
   for (i = 0; i < n; i++) P[i] = o_from_spt(&prims[i]);
   S.prims = P; S.n = n; S.light_id = 6; S.nee = nee & 1; S.uniform = (nee >> 1) & 1; S.g = &g;
+  S.vertices = S.misses = 0;
   o_srand(&g, seed);
   spt_oracle_camera(cam, lf, la, up, 65, (float)w / (float)h);
   origin = dv3(cam[0], cam[1], cam[2]);
@@ -287,7 +294,7 @@ int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp
   ver = dv3(cam[9], cam[10], cam[11]);
   for (y = 0, i = 0; y < h; y++) {
     unsigned short x, Xi[3];
-    Xi[0] = 0; Xi[1] = 0; Xi[2] = (unsigned short)(y * y * y);
+    Xi[0] = 0; Xi[1] = (nee & 4) ? (unsigned short)seed : 0; Xi[2] = (unsigned short)(y * y * y);
     for (x = 0; x < w; x++) {
       dv r = dv3(0, 0, 0);
       int s;
@@ -304,8 +311,13 @@ int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp
       i++;
     }
   }
+  if (stats) { stats[0] = S.vertices; stats[1] = S.misses; }
   free(P);
   return 0;
+}
+int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp, unsigned seed,
+                             int nee, double* c_out) {
+  return spt_oracle_compat_render_stats(prims, n, w, h, spp, seed, nee, c_out, NULL);
 }
 
 /* toInt :319-321 + the P3 writer :548-551 (byte-identical format). */
@@ -818,6 +830,29 @@ static inline uint64_t c_fix(float L, float inv_spp) {
   return v >= 0.0f ? (uint64_t)(uint32_t)v : 0u;
 }
 
+/* Contract: the fp32 plane coordinate of a rectangle. The reference has no epsilon on rectangles
+ * (:103-106), so a hit point rounded to the far side of its plane self-hits and the path leaks out
+ * of the room. How often the computed x = o + d*((k-o)/d) lands beyond k depends on the last
+ * significand bit of k at the working precision (measured: odd 2.4 %, even 0.09 % of hits, in
+ * fp32 and fp64 alike). k exactly representable in fp32: used as is (same statistics as fp64).
+ * Otherwise the neighbouring float whose last significand bit equals the double's: (float)81.6
+ * rounds to an odd significand where the double 81.6 is even, which made the fp32 ceiling leak 26x
+ * as often as the reference's and darkened the image by 0.5 %. */
+float spt_oracle_plane_k(double k) {
+  const float f = (float)k;
+  int e32, e64;
+  double m32, m64;
+  if ((double)f == k || !isfinite(k)) return f;
+  m32 = frexp((double)f, &e32); /* f = m32 * 2^e32, 0.5 <= |m32| < 1 */
+  m64 = frexp(k, &e64);
+  {
+    const uint32_t bit32 = (uint32_t)(uint64_t)ldexp(fabs(m32), 24) & 1u;
+    const uint32_t bit64 = (uint32_t)(uint64_t)ldexp(fabs(m64), 53) & 1u;
+    if (bit32 == bit64) return f;
+  }
+  return nextafterf(f, (double)f < k ? INFINITY : -INFINITY);
+}
+
 static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
   int i;
   for (i = 0; i < n; i++) {
@@ -830,7 +865,7 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
     } else {
       c_rect_mid(s[i].geom[0], s[i].geom[1], &P->ma, &P->ha);
       c_rect_mid(s[i].geom[2], s[i].geom[3], &P->mb, &P->hb);
-      P->k = (float)s[i].geom[4];
+      P->k = spt_oracle_plane_k(s[i].geom[4]);
     }
     P->e = fv3((float)s[i].e[0], (float)s[i].e[1], (float)s[i].e[2]);
     P->c = fv3((float)s[i].c[0], (float)s[i].c[1], (float)s[i].c[2]);

@@ -11,9 +11,48 @@ namespace spt {
 
 struct CRect { float k, ma, ha, mb, hb; int idx; };
 
+constexpr double pow2i(int e) {
+  double r = 1;
+  for (; e > 0; --e) r *= 2;
+  for (; e < 0; ++e) r *= 0.5;
+  return r;
+}
+constexpr int floor_log2(double a) {  // a > 0, finite
+  int e = 0;
+  for (; a >= 2; a *= 0.5) ++e;
+  for (; a < 1; a *= 2) --e;
+  return e;
+}
+// Last bit of the prec-bit significand of a normal a != 0.
+constexpr unsigned last_sig_bit(double a, int prec) {
+  a = a < 0 ? -a : a;
+  return (unsigned)((unsigned long long)(a * pow2i(prec - 1 - floor_log2(a))) & 1ull);
+}
+
+// The contract's fp32 plane coordinate of a rectangle (oracle spt_oracle_plane_k):
+// k itself when fp32 holds it exactly, otherwise the neighbouring float whose last significand bit
+// equals the double's. The reference has no epsilon on rectangles (:103-106); how often a hit point
+// rounds to the far side of its plane (and the path leaks out) follows that last bit — round-to-
+// nearest (float)81.6 is odd where the double is even, and leaked 26x as often at the ceiling.
+constexpr float plane_k(double k) {
+  const float f = (float)k;
+  if ((double)f == k || !(k - k == 0) || !(k > 0x1p-100 || k < -0x1p-100) || k > 0x1p100 ||
+      k < -0x1p100)
+    return f;
+  if (last_sig_bit((double)f, 24) == last_sig_bit(k, 53)) return f;
+  const double af = f < 0 ? -(double)f : (double)f;
+  const bool outward = ((double)f < k) == (f > 0);  // step away from zero?
+  double ulp = pow2i(floor_log2(af) - 23);
+  if (!outward && af == pow2i(floor_log2(af))) ulp *= 0.5;  // below a power of two
+  return (float)((double)f + ((double)f < k ? ulp : -ulp));
+}
+static_assert(plane_k(81.6) == 81.600006103515625f && plane_k(81.5) == 81.5f &&
+                  plane_k(-81.6) == -81.600006103515625f && plane_k(0.1) == 0.099999994039535522f,
+              "plane_k");
+
 // Same rounding as build_geo()/rect_mid() on the host: bounds rounded once from double.
 constexpr CRect crect(double a1, double a2, double b1, double b2, double k, int idx) {
-  return CRect{(float)k, (float)((a1 + a2) * 0.5), a2 >= a1 ? (float)((a2 - a1) * 0.5) : -1.0f,
+  return CRect{plane_k(k), (float)((a1 + a2) * 0.5), a2 >= a1 ? (float)((a2 - a1) * 0.5) : -1.0f,
                (float)((b1 + b2) * 0.5), b2 >= b1 ? (float)((b2 - b1) * 0.5) : -1.0f, idx};
 }
 

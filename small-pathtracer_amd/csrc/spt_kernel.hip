@@ -795,7 +795,7 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
       P.w1 = (float)s[i].geom[1]; P.w2 = (float)s[i].geom[2]; P.w3 = (float)s[i].geom[3];
       P.w4 = r * r;
     } else {
-      P.w1 = (float)s[i].geom[4];
+      P.w1 = plane_k(s[i].geom[4]);  // contract plane coordinate (spt_cornell.h)
       P.w2 = (float)s[i].geom[0]; P.w3 = (float)s[i].geom[1];
       P.w4 = (float)s[i].geom[2]; P.w5 = (float)s[i].geom[3];
     }
@@ -824,7 +824,7 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
     for (int i = 0; i < n; ++i) {
       if (s[i].kind != kinds[k]) continue;
       GeoRect& R = g->rect[r++];
-      R.k = (float)s[i].geom[4];
+      R.k = plane_k(s[i].geom[4]);
       rect_mid(s[i].geom[0], s[i].geom[1], &R.ma, &R.ha);
       rect_mid(s[i].geom[2], s[i].geom[3], &R.mb, &R.hb);
       R.idx = i;

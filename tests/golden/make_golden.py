@@ -8,6 +8,11 @@ runs it, and stores:
                                the build recipe, known-answer values, and counter-mode md5s
   counter_64x48_s16_{nee,cos}.npy  counter-mode contract images from oracle/ (regression pins for
                                the GPU kernel; produced by the oracle, not by the reference)
+  ref_fidelity_256x192_s256.npz  the reference's estimator statistics (P2 fixture): 16 runs each of
+                               oracle/_ref/smallpt_{nee,cos}_xs (row streams seeded too, so the runs
+                               are independent) at 256x192@256, seeds 101..116, as 16x16-block means
+                               of the linearised PPM ((v/255)^2.2): per-seed block means
+                               {est}_blocks (16, 12, 16, 3)
 """
 import hashlib
 import json
@@ -24,6 +29,33 @@ sys.path.insert(0, ROOT)
 
 def md5(path):
     return hashlib.md5(open(path, "rb").read()).hexdigest()
+
+
+def read_ppm(path):
+    tok = open(path, "rb").read().split()
+    w, h = int(tok[1]), int(tok[2])
+    return np.array(tok[4:4 + w * h * 3], dtype=np.float64).reshape(h, w, 3)
+
+
+def fidelity_fixture(ref, tmp, w=256, h=192, spp=256, seeds=range(101, 117), k=16):
+    """16x16-block means of the reference's linearised PPMs, one set per independent seed."""
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = [(est, s) for est in ("nee", "cos") for s in seeds]
+
+    def run(job):
+        est, s = job
+        path = os.path.join(tmp, f"fid_{est}_{s}.ppm")
+        subprocess.run([os.path.join(ref, f"smallpt_{est}_xs"), str(w), str(h), str(spp), str(s), path],
+                       check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        lin = (read_ppm(path) / 255.0) ** 2.2
+        return lin.reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+
+    with ThreadPoolExecutor(max(1, (os.cpu_count() or 2) - 1)) as ex:
+        blocks = list(ex.map(run, jobs))
+    n = len(seeds)
+    np.savez(os.path.join(HERE, f"ref_fidelity_{w}x{h}_s{spp}.npz"),
+             nee_blocks=np.array(blocks[:n]), cos_blocks=np.array(blocks[n:]),
+             seeds=np.array(list(seeds)), shape=np.array([w, h, spp, k]))
 
 
 def main():
@@ -45,6 +77,13 @@ def main():
             if w == 64:
                 with open(path, "rb") as f, open(os.path.join(HERE, os.path.basename(path)), "wb") as g:
                     g.write(f.read())
+    # Row-seeded variants (statistics builds): their PPMs pin oracle.compat_render(row_seed=True).
+    for est in ("nee", "cos"):
+        path = os.path.join(tmp, f"ref_xs_64x48_s4_seed5_{est}.ppm")
+        subprocess.run([os.path.join(ref, f"smallpt_{est}_xs"), "64", "48", "4", "5", path],
+                       check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        out["reference_md5"][f"xs_64x48_s4_seed5_{est}"] = md5(path)
+    fidelity_fixture(ref, tmp)
     # Known answers (measured by calling the reference's own functions).
     out["kat"] = {
         "camera_aspect1": {"llc": [49.362929701805115, 39.362929701805115, 167],

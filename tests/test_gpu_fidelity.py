@@ -1,0 +1,29 @@
+"""P2 on the MI355X: the product (HIP kernel through the C ABI, every kernel specialisation) against
+16 independent runs of the reference binary itself, pinned in tests/golden/ref_fidelity_256x192_s256.npz
+(tests/fidelity.py has the statistics and their calibration). The reference is not needed here.
+
+P1 (bit-exact with the CPU contract) says the GPU computes the contract; this says the contract,
+as the GPU runs it, estimates the same image as the reference (`smallpt.cpp:528-542`).
+"""
+import numpy as np
+import pytest
+
+import fidelity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kernel", ["const", "cornell", "generic"])
+@pytest.mark.parametrize("est", ["nee", "cos"])
+def test_product_estimates_the_reference_image(spt, monkeypatch, est, kernel):
+    monkeypatch.setenv("SPT_KERNEL", kernel)
+    fx = fidelity.load_fixture()
+    w, h, spp, k = fx["w"], fx["h"], fx["spp"], fx["k"]
+    own = []
+    for seed in range(1, 17):
+        p = spt.default_params(width=w, height=h, spp=spp, seed=seed, nee_prob=1.0 if est == "nee" else 0.0)
+        img = spt.render(spt.cornell_scene(), spt.Camera(aspect=w / h), p)
+        own.append(fidelity.blocks(img, k))
+    zg, z2 = fidelity.compare(fx[est], own)
+    assert np.all(np.abs(zg) < fidelity.GLOBAL_Z_MAX), zg
+    assert z2 < fidelity.BLOCK_Z2_MAX, z2
