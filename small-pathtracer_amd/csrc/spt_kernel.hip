@@ -49,7 +49,7 @@ struct alignas(16) DevPrim {
   int kind;
   float w1, w2, w3, w4, w5;
   int refl;  // spt_refl
-  float pad1;
+  float ip;  // 1/pmax, correctly rounded on the host (the RR reweighting f * (1/p) of :451)
   float ex, ey, ez, pmax;
   float cx, cy, cz, pad2;
 };
@@ -134,6 +134,22 @@ struct Topo {
 using TopoCornell = Topo<6, 5, 6, false, 8>;     // rect[] of :287-311 (light = XZ #3 -> pos 8)
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
+
+// Estimator configuration the kernel is specialised for (compile-time where the host can prove
+// it, -1 = read from KParams at run time). Only wave-uniform branches and parameter loads go away;
+// per lane the arithmetic is the same contract.
+//   NEE:   1 = nee_prob >= 1 (HEAD :464), 0 = nee_prob <= 0 (cosine only, :474-477)
+//   LMODE: light sampling (SPT_LIGHT_GLIBC_WRAP / SPT_LIGHT_UNIFORM)
+//   BLACK: 1 = the light's colour is 0, so a path reaching it ends there (RR with p == 0, :448)
+//   MAXD0: 1 = no hard depth cap (max_depth == 0, the reference)
+//   NOS1:  1 = no vertex-1 stream-1 draws (rr_depth >= 1 and nee_prob is 0 or 1)
+template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_>
+struct Cfg {
+  static constexpr int NEE = NEE_, LMODE = LMODE_, BLACK = BLACK_, MAXD0 = MAXD0_, NOS1 = NOS1_;
+};
+using CfgRuntime = Cfg<-1, -1, -1, -1, -1>;
+using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
+using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1>;  // C2: cosine-weighted only
 template <class TP>
 __device__ __forceinline__ auto rects_of(const SPT_CONST SceneGeo* G) {
   if constexpr (TP::CONSTGEO) return CornellRectPtr{0};
@@ -309,7 +325,7 @@ __device__ __forceinline__ T opq(T v) {
 //   iteration: [retire / refill units] -> [generate: cosine continuation or camera ray, one
 //   Philox call, shared normalize] -> [trace] -> [resolve a shadow ray] -> [shade a vertex: RR,
 //   NEE pre-test] -> [path end: accumulate].
-template <class TP>
+template <class TP, class CF>
 __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
@@ -338,7 +354,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   uint32_t branch = 0;    // path-tree position of a REFR split (counter word 2 bits 24+; MAT only)
   int sp = 0;             // pending refraction children in s_stack (MAT only)
   uint32_t lp = 0, s = 0, s_end = 0, pix = 0;
-  int px = 0, py = 0, depth = 0, vid = 0;
+  int depth = 0, vid = 0;
+  float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5), (h - y - 1 - 0.5) of :533-534
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
   f3 o = mk(0, 0, 0), d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
   u4 r = u4{0, 0, 0, 0};  // Philox words of the vertex the pending path ray leads to
@@ -396,11 +413,13 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         s = j * (uint32_t)Q->chunk;
         s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
         const uint32_t lr = div_magic(lp, Q->m_w, Q->sh_w);
-        px = (int)(lp - lr * w);
+        const int px = (int)(lp - lr * w);
         const uint32_t T_ = (uint32_t)Q->tile_rows;
         const uint32_t tile = div_magic(lr, Q->m_tile, Q->sh_tile), within = lr - tile * T_;
-        py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
+        const int py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
         pix = (uint32_t)py * w + (uint32_t)px;
+        fx = (float)px - 0.5f;
+        fy = (float)(Q->height - py - 1) - 0.5f;
         has_unit = true;
         needs_unit = false;
         gen = true;
@@ -437,8 +456,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       if (!cont) {
         SPT_REGION(3);
         const SPT_CONST KParams* C = cptr(Pg);
-        const float su = (((float)px - 0.5f) + u16(r.x, r.y)) * C->inv_w;
-        const float sv = (((float)(C->height - py - 1) - 0.5f) + u16(r.z, r.w)) * C->inv_h;
+        const float su = (fx + u16(r.x, r.y)) * C->inv_w;
+        const float sv = (fy + u16(r.z, r.w)) * C->inv_h;
         o = mk(C->cam[0], C->cam[1], C->cam[2]);
         v = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
                fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
@@ -483,7 +502,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           // The light hit by this very ray is the next vertex, shaded in the common block below.
           // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
           // random draw; anything else is shaded with that vertex's own Philox words.
-          if (!(hit && s_prims[id].pmax == 0.0f))
+          if (CF::BLACK != 1 && !(hit && s_prims[id].pmax == 0.0f))
             r = philox4x32_10(pix, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u), D->seed);
           vertex = true;
         } else {
@@ -500,6 +519,21 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const DevPrim& H = s_prims[id];
         const int kind = H.kind;
         f3 x;
+        f3 gn = mk(0, 0, 0);
+        if constexpr (!TP::SPH) {
+          // Rect-only scenes, branch-free: the plane axis of the hit kind selects (o_a, d_a); the
+          // hit point re-derives t = (k - o_a) / d_a as the reference does (:103) and
+          // the normal is the axis, oriented against the ray (:123,:166,:209).
+          const bool kxy = kind == SPT_RECT_XY, kxz = kind == SPT_RECT_XZ, kyz = !kxy && !kxz;
+          const float oa = kxy ? o.z : (kxz ? o.y : o.x);
+          const float da = kxy ? d.z : (kxz ? d.y : d.x);
+          const float tr = (H.w1 - oa) / da;
+          x = hit ? mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr) : mk(0, 0, 0);
+          e_miss = !hit;
+          const float sg = da < 0.0f ? 1.0f : -1.0f;
+          nl = mk(kyz ? sg : 0.0f, kxz ? sg : 0.0f, kxy ? sg : 0.0f);
+          if (TP::MAT) gn = mk(kyz ? 1.0f : 0.0f, kxz ? 1.0f : 0.0f, kxy ? 1.0f : 0.0f);
+        } else {
         if (!hit) {
           x = mk(0, 0, 0);
           e_miss = true;
@@ -512,7 +546,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         }
         // Hitable::normal, oriented against the ray (:123,:166,:209,:251); gn = the unoriented
         // (geometric) normal `n` of the SPEC/REFR code :482-491 (MAT only)
-        f3 gn = mk(0, 0, 0);
         if (kind == SPT_RECT_XY) {
           nl = d.z < 0.0f ? mk(0, 0, 1) : mk(0, 0, -1);
           if (TP::MAT) gn = mk(0, 0, 1);
@@ -527,18 +560,19 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
           if (TP::MAT) gn = n;
         }
+        }
         f3 f = mk(H.cx, H.cy, H.cz);
         const f3 e = mk(H.ex, H.ey, H.ez);
         const float p = H.pmax;
         ++depth;
         u4 rl = r;  // RR / NEE-mix draws; at vertex 1 from stream 1 (only configs that need them)
-        if (depth == 1) {
+        if (CF::NOS1 != 1 && depth == 1) {
           const SPT_CONST KParams* C = cptr(Pg);
           if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
             rl = philox4x32_10(pix, s, 1u | 0x80000000u, C->seed);
         }
         // Russian roulette :448-454 (+ optional hard depth cap).
-        const int max_depth = P->max_depth;
+        const int max_depth = CF::MAXD0 == 1 ? 0 : P->max_depth;
         if (max_depth > 0 && depth >= max_depth) {
           term = true;
         } else if (depth > P->rr_depth || p == 0.0f) {
@@ -548,7 +582,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
             bool keep = true;
             if (p < 1.0f) keep = u16(rl.x, rl.y) < p;
             if (keep) {
-              const float ip = 1.0f / p;
+              const float ip = H.ip;  // == 1.0f / p
               f = mk(f.x * ip, f.y * ip, f.z * ip);
             } else {
               term = true;
@@ -608,16 +642,23 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
           o = x;
           const SPT_CONST KParams* D = cptr(Pg);
-          const float q = D->nee_prob;
           bool nee;
-          if (q >= 1.0f) nee = true;
-          else if (q <= 0.0f) nee = false;
-          else nee = u16(rl.z, rl.w) < q;
+          if constexpr (CF::NEE == 1) {
+            nee = true;
+          } else if constexpr (CF::NEE == 0) {
+            nee = false;
+          } else {
+            const float q = D->nee_prob;
+            if (q >= 1.0f) nee = true;
+            else if (q <= 0.0f) nee = false;
+            else nee = u16(rl.z, rl.w) < q;
+          }
           bool cand = false;
           if (nee) {
             // light_sampling :363-369 and the shadow-ray direction :466.
             float xl, zl;
-            if (D->light_mode == SPT_LIGHT_GLIBC_WRAP) {
+            const int lmode = CF::LMODE >= 0 ? CF::LMODE : D->light_mode;
+            if (lmode == SPT_LIGHT_GLIBC_WRAP) {
               xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * D->ldxi), 0x1p-31f, D->lx0);
               zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * D->ldzi), 0x1p-31f, D->lz0);
             } else {
@@ -732,11 +773,18 @@ static spt_status fail(spt_status s, const std::string& msg) {
                   std::string(#call) + ": " + hipGetErrorString(e_));                    \
   } while (0)
 
+// Kernel variants, from the most general to the most specialised (SPT_KERNEL caps the level).
+using RenderFn = void (*)(const KParams*);
+enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_COUNT };
+static const RenderFn kRenderKernels[KV_COUNT] = {
+    render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
+    render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
+    render_kernel<TopoCornellConst, CfgHeadCos>};
+
 struct spt_context {
   int device = 0;
   int n_cu = 0, blocks_per_cu = 0;      // generic kernel
-  int blocks_per_cu_cornell = 0;        // TopoCornell specialisation
-  int blocks_per_cu_const = 0;          // TopoCornellConst (compile-time HEAD geometry)
+  int bpc[KV_COUNT] = {};               // resident blocks per CU of each variant
   DevPrim* prims = nullptr;
   SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
@@ -802,6 +850,7 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
     P.ex = (float)s[i].e[0]; P.ey = (float)s[i].e[1]; P.ez = (float)s[i].e[2];
     P.cx = (float)s[i].c[0]; P.cy = (float)s[i].c[1]; P.cz = (float)s[i].c[2];
     P.pmax = P.cx > P.cy && P.cx > P.cz ? P.cx : P.cy > P.cz ? P.cy : P.cz;  // :447
+    P.ip = 1.0f / P.pmax;  // IEEE single division, as the device's 1.0f / p
     P.refl = s[i].refl;
     out[i] = P;
   }
@@ -882,21 +931,14 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   spt_context* c = new spt_context();
   c->device = device;
   c->n_cu = prop.multiProcessorCount;
-  int bpc = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel<TopoGeneric>, kBlock, 0) !=
-          hipSuccess || bpc <= 0)
-    bpc = 4;
-  c->blocks_per_cu = bpc;
-  bpc = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel<TopoCornell>, kBlock, 0) !=
-          hipSuccess || bpc <= 0)
-    bpc = 4;
-  c->blocks_per_cu_cornell = bpc;
-  bpc = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, render_kernel<TopoCornellConst>, kBlock,
-                                                   0) != hipSuccess || bpc <= 0)
-    bpc = 4;
-  c->blocks_per_cu_const = bpc;
+  for (int v = 0; v < KV_COUNT; ++v) {
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kRenderKernels[v], kBlock, 0) !=
+            hipSuccess || bpc <= 0)
+      bpc = 4;
+    c->bpc[v] = bpc;
+  }
+  c->blocks_per_cu = c->bpc[KV_GENERIC];
   hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
   if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
@@ -1046,25 +1088,28 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   for (int i = 0; i < n_prims; ++i) all_diff = all_diff && prims[i].refl == SPT_DIFF;
   // The HEAD-topology kernels are all-DIFF, cosine-scatter specialisations; anything else (SPEC/
   // REFR, the uniform hemisphere) runs the generic kernel.
-  // SPT_KERNEL=generic|cornell (A/B and tests): cap the specialisation level.
+  // SPT_KERNEL=generic|cornell|const|head (A/B and tests): cap the specialisation level.
   const char* kenv = std::getenv("SPT_KERNEL");
-  const int kcap = !kenv ? 2 : std::strcmp(kenv, "generic") == 0 ? 0 : std::strcmp(kenv, "cornell") == 0 ? 1 : 2;
+  const int kcap = !kenv                               ? 3
+                   : std::strcmp(kenv, "generic") == 0 ? 0
+                   : std::strcmp(kenv, "cornell") == 0 ? 1
+                   : std::strcmp(kenv, "const") == 0   ? 2
+                                                       : 3;
   const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
                        g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
   const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
-  const int grid = c->n_cu * (cconst    ? c->blocks_per_cu_const
-                              : cornell ? c->blocks_per_cu_cornell
-                                        : c->blocks_per_cu);
+  // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
+  const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
+                        p->rr_depth >= 1;
+  int kv = KV_GENERIC;
+  if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
+  else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
+  else if (cconst) kv = KV_CONST;
+  else if (cornell) kv = KV_CORNELL;
+  const int grid = c->n_cu * c->bpc[kv];
   SPT_HIP(hipEventRecord(c->ev0, stream));
-  if (cconst)
-    hipLaunchKernelGGL(render_kernel<TopoCornellConst>, dim3(grid), dim3(kBlock), 0, stream,
-                       (const KParams*)c->d_kp);
-  else if (cornell)
-    hipLaunchKernelGGL(render_kernel<TopoCornell>, dim3(grid), dim3(kBlock), 0, stream,
-                       (const KParams*)c->d_kp);
-  else
-    hipLaunchKernelGGL(render_kernel<TopoGeneric>, dim3(grid), dim3(kBlock), 0, stream,
-                       (const KParams*)c->d_kp);
+  hipLaunchKernelGGL(kRenderKernels[kv], dim3(grid), dim3(kBlock), 0, stream,
+                     (const KParams*)c->d_kp);
   SPT_HIP(hipGetLastError());
   SPT_HIP(hipEventRecord(c->ev1, stream));
   const uint32_t n = 3u * (uint32_t)K.n_local_pix;

@@ -13,7 +13,7 @@ import fidelity
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kernel", ["const", "cornell", "generic"])
+@pytest.mark.parametrize("kernel", ["head", "const", "cornell", "generic"])
 @pytest.mark.parametrize("est", ["nee", "cos"])
 def test_product_estimates_the_reference_image(spt, monkeypatch, est, kernel):
     monkeypatch.setenv("SPT_KERNEL", kernel)

@@ -84,11 +84,12 @@ def test_specular_refractive_scene_bit_exact(spt, oracle, case):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
-@pytest.mark.parametrize("kernel", ["generic", "cornell"])
+@pytest.mark.parametrize("kernel", ["generic", "cornell", "const", "head"])
 @pytest.mark.parametrize("est,q,fl", [("nee", 1.0, 0), ("cos", 0.0, 0)])
 def test_every_kernel_specialisation_bit_exact(spt, oracle, monkeypatch, kernel, est, q, fl):
-    """The HEAD scene through the generic kernel and the runtime-geometry Cornell kernel too
-    (the default run takes the compile-time-geometry kernel): same contract, same bits."""
+    """The HEAD scene through every kernel variant: generic, runtime-geometry Cornell, compile-time
+    geometry with run-time estimator parameters, and the default compile-time estimator kernels
+    (HEAD NEE / cosine): same contract, same bits."""
     monkeypatch.setenv("SPT_KERNEL", kernel)
     p = spt.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
     gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
