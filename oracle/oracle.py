@@ -44,6 +44,7 @@ def lib() -> ctypes.CDLL:
         L.spt_oracle_erand48.restype = ctypes.c_double
         L.spt_oracle_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, P(ctypes.c_int32)]
         L.spt_oracle_philox.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
+        L.spt_oracle_set_pairs.argtypes = [ctypes.c_int]
         L.spt_oracle_sincos2pi.argtypes = [ctypes.c_float, P(ctypes.c_float), P(ctypes.c_float)]
         L.spt_oracle_camera.argtypes = [P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double),
                                         P(ctypes.c_double), ctypes.c_float, ctypes.c_float]
@@ -117,6 +118,11 @@ def counter_render(prims, cam, params, rows=None, threads: int = 0):
                                     rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(rows),
                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), st, threads)
     return out, dict(zip(_spt.STAT_KEYS, [int(v) for v in st]))
+
+
+def set_pairs(on: bool) -> None:
+    """Test hook: parallel-pair rect tests on (the contract) or off (every rect on its own)."""
+    lib().spt_oracle_set_pairs(1 if on else 0)
 
 
 def write_ppm(path: str, rgb: np.ndarray) -> None:

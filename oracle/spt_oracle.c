@@ -527,60 +527,125 @@ static void c_rect_mid(double lo, double hi, float* mid, float* half) {
   *half = hi >= lo ? (float)((hi - lo) * 0.5) : -1.0f;
 }
 
+/* One rectangle test of the counter-mode intersection: a single rectangle (k0 == k1, id0 == id1) or
+ * a PARALLEL PAIR — two rectangles of one kind with bit-identical in-plane bounds on different
+ * planes k0 < k1 (a box's opposite faces, the room's opposite walls). Per ray only the pair's plane
+ * that can be hit first is tested (c_intersect). */
+typedef struct {
+  int kind;
+  float k0, k1, ma, ha, mb, hb;
+  int id0, id1;
+} c_test;
+
 typedef struct {
   const c_prim* prims;
   int n;
   const spt_params* P;
   uint32_t key[2];
+  const c_test* tests; /* rect tests in contract order (c_build_tests) */
+  int n_tests;
 } c_ctx;
 
+/* Contract: the rect test list. Kinds in the order XY, XZ, YZ; inside a kind, rectangles in index
+ * order, each paired with the first later unpaired rectangle of its kind whose (ma, ha, mb, hb) are
+ * bit-identical and whose plane differs (a test is ordered by its first member's index). The light
+ * (P->light_id) is never paired. Returns the number of tests written to T (<= n). */
+static int g_pairs = 1;
+/* Test hook: 0 = no pairing (every rectangle tested on its own: the per-rectangle form the pair
+ * rule must reproduce), 1 = the contract. Not thread-safe against a running render. */
+void spt_oracle_set_pairs(int on) { g_pairs = on != 0; }
+static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
+  int used[64] = {0}, nt = 0, kind, i, j;
+  for (kind = SPT_RECT_XY; kind <= SPT_RECT_YZ; kind++) {
+    for (i = 0; i < n; i++) {
+      const c_prim* A = &P[i];
+      c_test* t;
+      if (A->kind != kind || used[i]) continue;
+      used[i] = 1;
+      t = &T[nt++];
+      t->kind = kind;
+      t->k0 = t->k1 = A->k;
+      t->ma = A->ma; t->ha = A->ha; t->mb = A->mb; t->hb = A->hb;
+      t->id0 = t->id1 = i;
+      if (i == light_id) continue;
+      if (!g_pairs) continue; /* diagnostic: every rectangle tested on its own */
+      for (j = i + 1; j < n; j++) {
+        const c_prim* B = &P[j];
+        if (B->kind != kind || used[j] || j == light_id) continue;
+        if (asu(B->ma) != asu(A->ma) || asu(B->ha) != asu(A->ha) || asu(B->mb) != asu(A->mb) ||
+            asu(B->hb) != asu(A->hb) || asu(B->k) == asu(A->k) || !(B->k == B->k) || !(A->k == A->k))
+          continue;
+        used[j] = 1;
+        if (A->k < B->k) { t->k1 = B->k; t->id1 = j; }
+        else { t->k0 = B->k; t->id0 = j; t->k1 = A->k; t->id1 = i; }
+        break;
+      }
+    }
+  }
+  return nt;
+}
+
 /* The counter-mode scene intersection (intersect :323-335). inv = rcp_nr(d) once per ray.
- * Primitives are tested grouped by kind — all RECT_XY in index order, then RECT_XZ, RECT_YZ,
- * SPHERE — with the reference's strict `<` (:328), so the first primitive in THAT order wins a
+ * The rect tests (c_build_tests) run in their contract order — kind XY, XZ, YZ — then the spheres
+ * in index order, with the reference's strict `<` (:328), so the first test in THAT order wins a
  * tie of exactly equal t (the reference: lowest index; they differ only for bit-identical t from
- * two different kinds). id is left untouched on a miss; returns 1 on hit, *t = 1e20f on a miss. */
+ * two different planes). id is left untouched on a miss; returns 1 on hit, *t = 1e20f on a miss.
+ *
+ * A parallel pair tests one plane per ray: with n_i = k_i - o_a, the plane k0 when the ray moves
+ * up the axis (inv_a > 0) from below it (n0 > 0), or down the axis (inv_a <= 0, incl. NaN) from
+ * anywhere not above k1 (n1 >= 0); otherwise k1. That is the plane of the pair that is ahead and
+ * nearer; the other one can only be the nearest hit of the two through the box's interior, i.e.
+ * when the first plane's test is missed within an ulp of an edge. Every test then computes
+ * t = n * inv_a exactly as a single rectangle (the same bits as testing that plane alone). */
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   const float ix = spt_oracle_rcp_nr(d.x), iy = spt_oracle_rcp_nr(d.y), iz = spt_oracle_rcp_nr(d.z);
   float tmin = 1e20f;
-  int kind, i;
-  for (kind = SPT_RECT_XY; kind <= SPT_SPHERE; kind++) {
-    for (i = 0; i < C->n; i++) {
-      const c_prim* P = &C->prims[i];
-      float tt, a, b;
-      if (P->kind != kind) continue;
-      switch (kind) {
-        case SPT_RECT_XY:
-          tt = (P->k - o.z) * iz; a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y); break;
-        case SPT_RECT_XZ:
-          tt = (P->k - o.y) * iy; a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z); break;
-        case SPT_RECT_YZ:
-          tt = (P->k - o.x) * ix; a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z); break;
-        default: { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
-          const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
-          const float bb = fdot(op, d);
-          const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-          const float det = P->rad2 - fdot(q, q);
-          float sd, t1, t2;
-          if (!(det >= 0.0f)) continue;
-          sd = sqrtf(det);
-          t1 = bb - sd;
-          t2 = bb + sd;
-          tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
-          if (tt != 0.0f && tt < tmin) { tmin = tt; *id = i; }
-          continue;
-        }
+  int i;
+  for (i = 0; i < C->n_tests; i++) {
+    const c_test* T = &C->tests[i];
+    float oa, ia, tt, a, b, n0, n1;
+    int sel1;
+    switch (T->kind) {
+      case SPT_RECT_XY: oa = o.z; ia = iz; break;
+      case SPT_RECT_XZ: oa = o.y; ia = iy; break;
+      default: oa = o.x; ia = ix; break;
+    }
+    n0 = T->k0 - oa;
+    n1 = T->k1 - oa;
+    sel1 = ia > 0.0f ? !(n0 > 0.0f) : (n1 < 0.0f);
+    tt = (sel1 ? n1 : n0) * ia;
+    switch (T->kind) {
+      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y); break;
+      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z); break;
+      default: a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z); break;
+    }
+    /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin:
+     * bounds as |a - mid| <= half per axis (c_rect_mid), 0 < t < tmin as one unsigned compare of the
+     * float bit patterns minus one (exact for every float incl. +-0, inf, NaN). */
+    {
+      const int inb = fabsf(a - T->ma) <= T->ha && fabsf(b - T->mb) <= T->hb;
+      const int trange = (asu(tt) - 1u) < (asu(tmin) - 1u);
+      if (inb && trange) {
+        tmin = tt;
+        *id = sel1 ? T->id1 : T->id0;
       }
-      /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin:
-       * bounds as |a - mid| <= half per axis (c_rect_mid), 0 < t < tmin as one unsigned compare of the
-       * float bit patterns minus one (exact for every float incl. +-0, inf, NaN). */
-      {
-        const int inb = fabsf(a - P->ma) <= P->ha && fabsf(b - P->mb) <= P->hb;
-        const int trange = (asu(tt) - 1u) < (asu(tmin) - 1u);
-        if (inb && trange) {
-          tmin = tt;
-          *id = i;
-        }
-      }
+    }
+  }
+  for (i = 0; i < C->n; i++) {
+    const c_prim* P = &C->prims[i];
+    if (P->kind != SPT_SPHERE) continue;
+    { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
+      const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
+      const float bb = fdot(op, d);
+      const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+      const float det = P->rad2 - fdot(q, q);
+      float sd, t1, t2, tt;
+      if (!(det >= 0.0f)) continue;
+      sd = sqrtf(det);
+      t1 = bb - sd;
+      t2 = bb + sd;
+      tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+      if (tt != 0.0f && tt < tmin) { tmin = tt; *id = i; }
     }
   }
   *t = tmin;
@@ -600,8 +665,11 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
     r2s = m * spt_oracle_rsq_nr(m);
     s1 = 1.0f - xi2;
   } else {
-    r2s = xi2 * spt_oracle_rsq_nr(xi2);
-    s1 = (1.0f - xi2) * spt_oracle_rsq_nr(1.0f - xi2);
+    /* (cos, sin) * sqrt(r2) and sqrt(1 - r2) (:343-347) scaled by 1 / sqrt(1 - r2): the direction
+       is normalized below anyway, so the contract takes R = sqrt(r2 / (1 - r2)) with ONE rsqrt,
+       R = r2 * rsq(r2 * (1 - r2)), and a normal component of exactly 1. */
+    r2s = xi2 * spt_oracle_rsq_nr(xi2 * (1.0f - xi2));
+    s1 = 1.0f;
   }
   cr = c * r2s;
   sr = s * r2s;
@@ -880,15 +948,20 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
 int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* cam,
                               const spt_params* P, const int32_t* rows, int nrows, float* rgb_out,
                               uint64_t* stats_out, int threads) {
-  c_prim* CP = (c_prim*)malloc(sizeof(c_prim) * (size_t)n);
+  c_prim* CP;
   c_ctx C;
+  c_test CT[64];
   float camf[12];
   const float inv_spp = 1.0f / (float)P->spp;
   c_stats tot;
   int i, ri;
+  if (n <= 0 || n > 64) return -1; /* the C ABI's limit (spt_render: n_prims in [1, 64]) */
+  CP = (c_prim*)malloc(sizeof(c_prim) * (size_t)n);
   memset(&tot, 0, sizeof tot);
   c_prims_from_spt(prims, n, CP);
   C.prims = CP; C.n = n; C.P = P; C.key[0] = SPT_PHILOX_KEY0; C.key[1] = SPT_PHILOX_KEY1;
+  C.n_tests = c_build_tests(CP, n, P->light_id, CT);
+  C.tests = CT;
   for (i = 0; i < 3; i++) {
     camf[i] = (float)cam->origin[i];
     camf[3 + i] = (float)cam->lower_left_corner[i];

@@ -69,4 +69,41 @@ constexpr CRect kCornellRects[17] = {
     crect(0, 50, 32, 62, 42, 10), crect(0, 25, 63, 88, 63, 14), crect(0, 25, 63, 88, 88, 15)};
 constexpr int kCornellNXY = 6, kCornellNXZ = 5, kCornellNYZ = 6, kCornellLightPos = 8;
 
+// The contract's rect tests over the grouped list (oracle c_build_tests): inside each kind group,
+// in order, a rectangle pairs with the first later unpaired one of bit-identical bounds on a
+// different plane (never the light); singles have k0 == k1, pos0 == pos1. axis: 2 = z (XY),
+// 1 = y (XZ), 0 = x (YZ). pos*: grouped positions.
+struct CTest { float k0, k1, ma, ha, mb, hb; int pos0, pos1, axis; };
+struct CTestList { CTest t[17]; int n; };
+constexpr bool same_bits(float a, float b) { return a == b && (a != 0.0f || (1.0f / a == 1.0f / b)); }
+constexpr CTestList cornell_tests() {
+  CTestList L{};
+  bool used[17] = {};
+  const int grp[4] = {0, kCornellNXY, kCornellNXY + kCornellNXZ, kCornellNXY + kCornellNXZ + kCornellNYZ};
+  for (int g = 0; g < 3; ++g) {
+    for (int i = grp[g]; i < grp[g + 1]; ++i) {
+      if (used[i]) continue;
+      used[i] = true;
+      const CRect& A = kCornellRects[i];
+      CTest t{A.k, A.k, A.ma, A.ha, A.mb, A.hb, i, i, 2 - g};
+      if (i != kCornellLightPos) {
+        for (int j = i + 1; j < grp[g + 1]; ++j) {
+          const CRect& B = kCornellRects[j];
+          if (used[j] || j == kCornellLightPos || !same_bits(A.ma, B.ma) || !same_bits(A.ha, B.ha) ||
+              !same_bits(A.mb, B.mb) || !same_bits(A.hb, B.hb) || same_bits(A.k, B.k))
+            continue;
+          used[j] = true;
+          if (A.k < B.k) { t.k1 = B.k; t.pos1 = j; }
+          else { t.k0 = B.k; t.pos0 = j; t.k1 = A.k; t.pos1 = i; }
+          break;
+        }
+      }
+      L.t[L.n++] = t;
+    }
+  }
+  return L;
+}
+constexpr CTestList kCornellTests = cornell_tests();
+static_assert(kCornellTests.n == 10, "HEAD scene: 7 parallel pairs + light + 2 box tops");
+
 }  // namespace spt

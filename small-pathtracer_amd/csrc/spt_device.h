@@ -123,9 +123,11 @@ __device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool u
     r2s = m * rsq_nr(m);
     s1 = 1.0f - xi2;
   } else {
-    r2s = xi2 * rsq_nr(xi2);  // sqrt(r2); xi2 = 0 gives 0
-    const float om = 1.0f - xi2;
-    s1 = om * rsq_nr(om);     // sqrt(1 - r2)
+    // Contract (oracle c_cosine): sqrt(r2) and sqrt(1 - r2) of :343-347 scaled by 1/sqrt(1 - r2),
+    // since the kernel normalizes the direction anyway: R = sqrt(r2 / (1 - r2)) with ONE rsqrt,
+    // R = r2 * rsq(r2 * (1 - r2)) (r2 = 0 gives 0), and a normal component of exactly 1.
+    r2s = xi2 * rsq_nr(xi2 * (1.0f - xi2));
+    s1 = 1.0f;
   }
   const float cr = c * r2s, sr = s * r2s;
   // Contract: an axis-aligned normal (every rectangle's, :123,:166,:209) makes the frame of

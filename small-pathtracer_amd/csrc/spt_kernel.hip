@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 
 #include "../../include/spt.h"
 #include "../../include/spt_flops.h"
@@ -29,11 +30,6 @@
 #include "spt_cornell.h"
 
 namespace spt {
-
-// Rect-test formulation (A/B): 0 = SALU mask logic, 1/2 = lane-mask selects (see rect_group).
-#ifndef SPT_RECT_FORM
-#define SPT_RECT_FORM 0
-#endif
 
 constexpr int kMaxPrims = 64;
 constexpr int kBlock = 256;
@@ -62,11 +58,15 @@ static_assert(sizeof(DevPrim) == 64, "DevPrim layout");
 // subtract + one compare, each reading a single SGPR (the VALU constant-bus limit on gfx950).
 struct GeoRect { float k, ma, ha, mb, hb; int idx; int pad0, pad1; };   // 32 B
 struct GeoSph { float px, py, pz, rad2; int idx; int pad0, pad1, pad2; };  // 32 B
+// A rect test of the contract (oracle c_test): a parallel pair (k0 < k1, shared bounds) or a single
+// (k0 == k1, pos0 == pos1); pos* are grouped positions in rect[].
+struct GeoTest { float k0, k1, ma, ha, mb, hb; int pos0, pos1; };      // 32 B
 struct SceneGeo {
   int n_xy, n_xz, n_yz, n_sph;
-  int pad[4];
+  int n_txy, n_txz, n_tyz, pad;  // rect tests per kind
   GeoRect rect[kMaxPrims];  // [0,n_xy) XY, [n_xy, n_xy+n_xz) XZ, then YZ
   GeoSph sph[kMaxPrims];
+  GeoTest test[kMaxPrims];  // [0,n_txy) XY, then XZ, then YZ
 };
 #define SPT_CONST __attribute__((address_space(4)))
 
@@ -126,12 +126,17 @@ struct CornellRectPtr {
 // bounds are the compile-time HEAD scene (CONSTGEO) or read from the uploaded scene (s_load).
 // MAT: SPEC/REFR materials and the uniform-hemisphere flag may occur (generic kernel); the
 // specialisations are all-DIFF, cosine-scatter scenes (keeps their cosine block branch-free).
-template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false>
+// NT*: rect tests per kind (parallel pairs count once).
+template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false,
+          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
+  static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = SPH_;
 };
-using TopoCornell = Topo<6, 5, 6, false, 8>;     // rect[] of :287-311 (light = XZ #3 -> pos 8)
+// rect[] of :287-311 (light = XZ #3 -> pos 8); tests: 3 XY pairs, XZ floor/ceiling pair + light +
+// 2 box tops, 3 YZ pairs
+using TopoCornell = Topo<6, 5, 6, false, 8, false, 3, 4, 3>;
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 
@@ -164,6 +169,100 @@ __device__ __forceinline__ Ray6 ray6(f3 o, f3 d, float ix, float iy, float iz) {
   return Ray6{o.x, ix, d.y, o.y, d.z, o.z};
 }
 
+// One rect test of the contract (oracle c_intersect). A parallel pair tests the plane that can be
+// hit first: k0 when the ray moves up the axis (inv_a > 0) from below it (n0 > 0) or down the axis
+// from anywhere not above k1 (n1 >= 0), else k1; t = n * inv_a as for a single rectangle.
+// v_cndmask with an explicit 64-bit lane mask: LLVM turns the pair rule's mask logic into a select
+// of booleans held in VGPRs (~6 VALU); as SALU operations on ballot masks it is free.
+__device__ __forceinline__ float sel_f(uint64_t m, float a, float b) {  // m ? b : a per lane
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+__device__ __forceinline__ int sel_i(uint64_t m, int a, int b) {
+  int r;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+template <int A, int B>  // compile-time positions as inline constants
+__device__ __forceinline__ int sel_ic(uint64_t m) {
+  int r;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "I"(A), "I"(B), "s"(m));
+  return r;
+}
+// Grouped position of the tested plane of a pair.
+struct GeoTest;
+template <int J> struct CornellTestPtr;
+template <int J>
+__device__ __forceinline__ int pair_pos(CornellTestPtr<J>, uint64_t sel1);
+__device__ __forceinline__ int pair_pos(const SPT_CONST GeoTest* g, uint64_t sel1);
+__device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// One rect test of the contract (oracle c_intersect). A parallel pair tests the plane that can be
+// hit first: k0 when the ray moves up the axis (inv_a > 0) from below it (n0 > 0) or down the axis
+// from anywhere not above k1 (n1 >= 0), else k1; t = n * inv_a as for a single rectangle.
+// up: lane mask of inv_a > 0.
+template <bool PAIR, class GP>
+__device__ __forceinline__ void rect_test(GP g, const Ray6& r, uint64_t up, uint32_t& tmin_key,
+                                          int& pos) {
+  const float n0 = g->k0 - r.oa;
+  float n = n0;
+  uint64_t sel1 = 0;
+  if constexpr (PAIR) {
+    const float n1 = g->k1 - r.oa;
+    sel1 = (up & ~lanes(n0 > 0.0f)) | (~up & lanes(n1 < 0.0f));
+    n = sel_f(sel1, n0, n1);
+  }
+  const float tt = n * r.ia;
+  const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
+  const bool inb = (bool)((int)(fabsf(a - g->ma) <= g->ha) & (int)(fabsf(b - g->mb) <= g->hb));
+  const uint32_t kk = tkey(tt);
+  const bool acc = inb & (kk < tmin_key);
+  tmin_key = acc ? kk : tmin_key;
+  if constexpr (PAIR) {
+    const int q = pair_pos(g, sel1);
+    pos = acc ? q : pos;
+  }
+  else pos = acc ? g->pos0 : pos;
+}
+
+// Compile-time HEAD tests (spt_cornell.h kCornellTests): every operand a literal.
+template <int J>
+struct CornellTestPtr {
+  __device__ constexpr const CTest* operator->() const { return &kCornellTests.t[J]; }
+};
+template <int J>
+__device__ __forceinline__ int pair_pos(CornellTestPtr<J>, uint64_t sel1) {
+  return sel_ic<kCornellTests.t[J].pos0, kCornellTests.t[J].pos1>(sel1);
+}
+__device__ __forceinline__ int pair_pos(const SPT_CONST GeoTest* g, uint64_t sel1) {
+  return sel_i(sel1, g->pos0, g->pos1);
+}
+template <int J>
+__device__ __forceinline__ void cornell_test(const Ray6* rays, const uint64_t* up, uint32_t& tmin_key,
+                                             int& pos) {
+  constexpr int ax = kCornellTests.t[J].axis;
+  constexpr bool pair = kCornellTests.t[J].pos0 != kCornellTests.t[J].pos1;
+  rect_test<pair>(CornellTestPtr<J>{}, rays[ax], up[ax], tmin_key, pos);
+}
+template <int... J>
+__device__ __forceinline__ void cornell_tests(std::integer_sequence<int, J...>, const Ray6* rays,
+                                              const uint64_t* up, uint32_t& tmin_key, int& pos) {
+  (cornell_test<J>(rays, up, tmin_key, pos), ...);
+}
+
+template <int N>  // the tests of one kind group, uploaded geometry (every test as a pair)
+__device__ __forceinline__ void test_group(const SPT_CONST GeoTest* g, int n_rt, const Ray6& r,
+                                           uint32_t& tmin_key, int& pos) {
+  const uint64_t up = lanes(r.ia > 0.0f);
+  if constexpr (N >= 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) rect_test<true>(g + j, r, up, tmin_key, pos);
+  } else {
+    for (int j = 0; j < n_rt; ++j) rect_test<true>(g + j, r, up, tmin_key, pos);
+  }
+}
+
 struct RectHit { float tt; bool inb; };
 template <class GP>
 __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
@@ -171,40 +270,6 @@ __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
   const bool ia = fabsf(a - g->ma) <= g->ha, ib = fabsf(b - g->mb) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib)};
-}
-
-template <int N, int AXIS, class GP>  // nearest-hit over one kind group
-__device__ __forceinline__ void rect_group(GP g, int n_rt, int pos0, const Ray6& r,
-                                           uint32_t& tmin_key, int& pos) {
-  auto one = [&](GP gj, int q) {
-#if SPT_RECT_FORM == 0
-    const RectHit h = rect_eval(gj, r);
-    const uint32_t kk = tkey(h.tt);
-    const bool acc = h.inb & (kk < tmin_key);
-    tmin_key = acc ? kk : tmin_key;
-    pos = acc ? q : pos;
-#else
-    // bounds folded into the key with lane-mask selects (no SALU mask logic, short chain)
-    const float tt = (gj->k - r.oa) * r.ia;
-    const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
-    const bool ia = fabsf(a - gj->ma) <= gj->ha, ib = fabsf(b - gj->mb) <= gj->hb;
-    uint32_t kk = tkey(tt);
-    kk = ia ? kk : 0xFFFFFFFFu;
-#if SPT_RECT_FORM == 1
-    asm volatile("" : "+v"(kk));
-#endif
-    kk = ib ? kk : 0xFFFFFFFFu;
-    const bool acc = kk < tmin_key;
-    tmin_key = acc ? kk : tmin_key;
-    pos = acc ? q : pos;
-#endif
-  };
-  if constexpr (N >= 0) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) one(g + j, pos0 + j);
-  } else {
-    for (int j = 0; j < n_rt; ++j) one(g + j, pos0 + j);
-  }
 }
 
 __device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d) {
@@ -229,14 +294,21 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
   uint32_t tmin_key = tkey(1e20f);
   int pos = -1;
-  const int nxy = n_of<TP>(TP::NXY, G->n_xy), nxz = n_of<TP>(TP::NXZ, G->n_xz);
-  const int nyz = n_of<TP>(TP::NYZ, G->n_yz);
-  rect_group<TP::NXY, 2>(rect, nxy, 0, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
-  rect_group<TP::NXZ, 1>(rect + nxy, nxz, nxy, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
-  rect_group<TP::NYZ, 0>(rect + nxy + nxz, nyz, nxy + nxz, ray6<0>(o, d, ix, iy, iz), tmin_key,
-                         pos);
+  if constexpr (TP::CONSTGEO) {
+    const Ray6 rays[3] = {ray6<0>(o, d, ix, iy, iz), ray6<1>(o, d, ix, iy, iz),
+                          ray6<2>(o, d, ix, iy, iz)};
+    const uint64_t up[3] = {lanes(ix > 0.0f), lanes(iy > 0.0f), lanes(iz > 0.0f)};
+    cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, up, tmin_key, pos);
+  } else {
+    const int ntxy = n_of<TP>(TP::NTXY, G->n_txy), ntxz = n_of<TP>(TP::NTXZ, G->n_txz);
+    const int ntyz = n_of<TP>(TP::NTYZ, G->n_tyz);
+    test_group<TP::NTXY>(G->test, ntxy, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
+    test_group<TP::NTXZ>(G->test + ntxy, ntxz, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
+    test_group<TP::NTYZ>(G->test + ntxy + ntxz, ntyz, ray6<0>(o, d, ix, iy, iz), tmin_key, pos);
+  }
+  (void)rect;
   if constexpr (TP::SPH) {
-    const int nsph = G->n_sph, base = nxy + nxz + nyz;
+    const int nsph = G->n_sph, base = G->n_xy + G->n_xz + G->n_yz;
     for (int j = 0; j < nsph; ++j) {
       const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
       const bool acc = kk < tmin_key;
@@ -881,6 +953,37 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
       ++*counts[k];
     }
   }
+  // Rect tests (oracle c_build_tests): inside each kind group, in order, a rectangle pairs with the
+  // first later unpaired one of bit-identical bounds on a different plane; the light never pairs.
+  {
+    bool used[kMaxPrims] = {};
+    const int grp[4] = {0, g->n_xy, g->n_xy + g->n_xz, g->n_xy + g->n_xz + g->n_yz};
+    int* tcounts[3] = {&g->n_txy, &g->n_txz, &g->n_tyz};
+    int nt = 0;
+    auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+    for (int k = 0; k < 3; ++k) {
+      for (int i = grp[k]; i < grp[k + 1]; ++i) {
+        if (used[i]) continue;
+        used[i] = true;
+        const GeoRect& A = g->rect[i];
+        GeoTest& T = g->test[nt++];
+        T = GeoTest{A.k, A.k, A.ma, A.ha, A.mb, A.hb, i, i};
+        ++*tcounts[k];
+        if (i == *light_pos) continue;
+        for (int j = i + 1; j < grp[k + 1]; ++j) {
+          const GeoRect& B = g->rect[j];
+          if (used[j] || j == *light_pos || bits(A.ma) != bits(B.ma) || bits(A.ha) != bits(B.ha) ||
+              bits(A.mb) != bits(B.mb) || bits(A.hb) != bits(B.hb) || bits(A.k) == bits(B.k) ||
+              !(A.k == A.k) || !(B.k == B.k))
+            continue;
+          used[j] = true;
+          if (A.k < B.k) { T.k1 = B.k; T.pos1 = j; }
+          else { T.k0 = B.k; T.pos0 = j; T.k1 = A.k; T.pos1 = i; }
+          break;
+        }
+      }
+    }
+  }
   for (int i = 0; i < n; ++i) {
     if (s[i].kind != SPT_SPHERE) continue;
     GeoSph& S = g->sph[g->n_sph++];
@@ -1096,7 +1199,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                    : std::strcmp(kenv, "const") == 0   ? 2
                                                        : 3;
   const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
-                       g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8;
+                       g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8 &&
+                       g.n_txy == 3 && g.n_txz == 4 && g.n_tyz == 3;
   const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
   // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
   const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&

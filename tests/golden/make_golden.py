@@ -2,7 +2,7 @@
 
 Builds oracle/_ref/smallpt_{nee,cos} from /root/reference/src/smallpt.cpp via oracle/build_ref.sh
 (the SURVEY.md Appendix A patch streamed through sed into g++ -O3; no reference source is copied),
-runs it, and stores:
+runs it, and stores (`--counter-only`: only the counter-mode pins, after a contract change):
   ref_64x48_s4_{nee,cos}.ppm   the reference's own output PPMs (data fixtures)
   golden.json                  md5s of the reference PPMs for 64x48@4 and 256x192@4 (NEE, cosine),
                                the build recipe, known-answer values, and counter-mode md5s
@@ -58,7 +58,31 @@ def fidelity_fixture(ref, tmp, w=256, h=192, spp=256, seeds=range(101, 117), k=1
              seeds=np.array(list(seeds)), shape=np.array([w, h, spp, k]))
 
 
+def counter_pins(out):
+    """Counter-mode contract pins (oracle output) for the GPU regression tests."""
+    from oracle import oracle as o
+    o.build()
+    prims = o.scene_cornell()
+    out["counter_md5"] = {}
+    out["counter_stats"] = {}
+    for est, q, fl in (("nee", 1.0, 0), ("cos", 0.0, 0), ("uni", 1.0, 1)):
+        p = o.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
+        img, st = o.counter_render(prims, o.camera(64 / 48), p)
+        if est != "uni":
+            np.save(os.path.join(HERE, f"counter_64x48_s16_{est}.npy"), img)
+        out["counter_md5"][est] = hashlib.md5(img.tobytes()).hexdigest()
+        out["counter_stats"][est] = st
+
+
 def main():
+    if "--counter-only" in sys.argv:  # contract change: re-pin the oracle's images, keep the rest
+        path = os.path.join(HERE, "golden.json")
+        out = json.load(open(path))
+        counter_pins(out)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out["counter_md5"], indent=1))
+        return
     if not os.path.exists("/root/reference/src/smallpt.cpp"):
         sys.exit("reference not present: golden fixtures can only be regenerated in the dev container")
     subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
@@ -103,18 +127,7 @@ def main():
              "out": [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]},
         ],
     }
-    # Counter-mode contract pins (oracle output) for the GPU regression tests.
-    from oracle import oracle as o
-    o.build()
-    prims = o.scene_cornell()
-    out["counter_md5"] = {}
-    for est, q, fl in (("nee", 1.0, 0), ("cos", 0.0, 0), ("uni", 1.0, 1)):
-        p = o.default_params(width=64, height=48, spp=16, seed=1, nee_prob=q, flags=fl)
-        img, st = o.counter_render(prims, o.camera(64 / 48), p)
-        if est != "uni":
-            np.save(os.path.join(HERE, f"counter_64x48_s16_{est}.npy"), img)
-        out["counter_md5"][est] = hashlib.md5(img.tobytes()).hexdigest()
-        out.setdefault("counter_stats", {})[est] = st
+    counter_pins(out)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["reference_md5"], indent=1))
