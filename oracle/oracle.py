@@ -45,6 +45,7 @@ def lib() -> ctypes.CDLL:
         L.spt_oracle_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, P(ctypes.c_int32)]
         L.spt_oracle_philox.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
         L.spt_oracle_set_pairs.argtypes = [ctypes.c_int]
+        L.spt_oracle_disk_dir.argtypes = [ctypes.c_uint32, P(ctypes.c_float), P(ctypes.c_float)]
         L.spt_oracle_sincos2pi.argtypes = [ctypes.c_float, P(ctypes.c_float), P(ctypes.c_float)]
         L.spt_oracle_camera.argtypes = [P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double),
                                         P(ctypes.c_double), ctypes.c_float, ctypes.c_float]
@@ -167,6 +168,13 @@ def philox(ctr, key):
     o = (ctypes.c_uint32 * 4)()
     lib().spt_oracle_philox(c, k, o)
     return list(o)
+
+
+def disk_dir(ra: int):
+    """(cos phi, sin phi) of the contract's azimuth from one Philox word (octant symmetry)."""
+    c, s = ctypes.c_float(), ctypes.c_float()
+    lib().spt_oracle_disk_dir(ctypes.c_uint32(ra), ctypes.byref(c), ctypes.byref(s))
+    return c.value, s.value
 
 
 def sincos2pi(xi: float):

@@ -509,6 +509,27 @@ void spt_oracle_sincos2pi(float xi, float* s_out, float* c_out) {
   }
 }
 
+/* The azimuth of random_scattering (:343, r1 = 2*pi*xi) in the contract: (cos phi, sin phi) from
+ * one 32-bit word by octant symmetry. Bits 31, 30 = signs of cos and sin, bit 29 = swap, bits 28..8
+ * = theta in [0, pi/4) (21 bits; theta = u * (pi/2) * 2^-22, the sincos2pi polynomials in quarter
+ * turns r = u * 2^-22 < 1/2). Uniform on the circle like 2*pi*xi (8 octants x 2^21 angles), without
+ * the quarter-turn reduction or a quadrant rotation. */
+void spt_oracle_disk_dir(uint32_t ra, float* c_out, float* s_out) {
+  const float r = (float)((ra >> 8) & 0x1FFFFFu) * 0x1p-22f;
+  const float r2 = r * r;
+  float ps = fmaf(r2, SC_S9, SC_S7), pc = fmaf(r2, SC_C8, SC_C6), sn, cs, t;
+  ps = fmaf(r2, ps, SC_S5);
+  ps = fmaf(r2, ps, SC_S3);
+  ps = fmaf(r2, ps, SC_S1);
+  sn = r * ps;
+  pc = fmaf(r2, pc, SC_C4);
+  pc = fmaf(r2, pc, SC_C2);
+  cs = fmaf(r2, pc, 1.0f);
+  if (ra & 0x20000000u) { t = cs; cs = sn; sn = t; }
+  *c_out = asf(asu(cs) ^ (ra & 0x80000000u));
+  *s_out = asf(asu(sn) ^ ((ra << 1) & 0x80000000u));
+}
+
 typedef struct {
   int kind;
   float k;                 /* rect: plane coordinate */
@@ -614,16 +635,18 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     n1 = T->k1 - oa;
     sel1 = ia > 0.0f ? !(n0 > 0.0f) : (n1 < 0.0f);
     tt = (sel1 ? n1 : n0) * ia;
+    /* In-plane offsets from the rectangle's centre: a = d_b * t + (o_b - mid_b) in one fma (the
+     * origin's offset o_b - mid_b is per ray, shared by every rectangle with that centre). */
     switch (T->kind) {
-      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x); b = fmaf(d.y, tt, o.y); break;
-      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x); b = fmaf(d.z, tt, o.z); break;
-      default: a = fmaf(d.y, tt, o.y); b = fmaf(d.z, tt, o.z); break;
+      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x - T->ma); b = fmaf(d.y, tt, o.y - T->mb); break;
+      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x - T->ma); b = fmaf(d.z, tt, o.z - T->mb); break;
+      default: a = fmaf(d.y, tt, o.y - T->ma); b = fmaf(d.z, tt, o.z - T->mb); break;
     }
     /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin:
-     * bounds as |a - mid| <= half per axis (c_rect_mid), 0 < t < tmin as one unsigned compare of the
+     * bounds as |a| <= half per axis (c_rect_mid), 0 < t < tmin as one unsigned compare of the
      * float bit patterns minus one (exact for every float incl. +-0, inf, NaN). */
     {
-      const int inb = fabsf(a - T->ma) <= T->ha && fabsf(b - T->mb) <= T->hb;
+      const int inb = fabsf(a) <= T->ha && fabsf(b) <= T->hb;
       const int trange = (asu(tt) - 1u) < (asu(tmin) - 1u);
       if (inb && trange) {
         tmin = tt;
@@ -655,11 +678,11 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
 /* random_scattering in the contract: cosine (:340-347), or with `uniform` the commented-out
    uniform hemisphere (:352-359): radial sqrt(r2*(2-r2)) and normal component (1-r2). */
 static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
-  const float xi1 = u01(ra), xi2 = u01(rb);
+  const float xi2 = u01(rb);
   float s, c;
   fv a, u, v;
   float r2s, s1, cr, sr;
-  spt_oracle_sincos2pi(xi1, &s, &c);
+  spt_oracle_disk_dir(ra, &c, &s); /* the azimuth r1 = 2*pi*xi1 of :343 */
   if (uniform) {
     const float m = xi2 * (2.0f - xi2);
     r2s = m * spt_oracle_rsq_nr(m);
@@ -699,6 +722,13 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
  * x = o + d*t lands relative to the plane sets the self-hit / leak rate (see spt_oracle_plane_k). */
 static float c_hit_t(float n, float da, float t) {
   return fmaf(fmaf(-t, da, n), spt_oracle_rcp_nr(da), t);
+}
+/* n / d in the contract where the reference divides once per event (the NEE pdf :471):
+ * q = n * rcp_nr(d) and one Markstein correction — the IEEE quotient in practice, without the
+ * device's ~30-cycle correctly rounded division sequence. */
+static float c_div(float n, float d) {
+  const float y = spt_oracle_rcp_nr(d), q = n * y;
+  return fmaf(fmaf(-q, d, n), y, q);
 }
 
 typedef struct {
@@ -876,7 +906,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         st->nee_events++;
         st->shadow_rays++;
         if (ids == P->light_id) {
-          const float pdf = fabsf((P->light_area * dl.y) / (ts * ts));
+          const float pdf = fabsf(c_div(P->light_area * dl.y, ts * ts));
           const float brdf = fabsf(fdot(dl, nl) * 0.318309886183790672f);
           st->nee_light_hits++;
           w = pdf * brdf;

@@ -107,6 +107,28 @@ __device__ __forceinline__ void sincos2pi(float xi, float& s_out, float& c_out) 
   c_out = (k == 1 || k == 2) ? -ca : ca;
 }
 
+// The azimuth of random_scattering (:343) from one Philox word by octant symmetry (oracle
+// spt_oracle_disk_dir): bits 31, 30 = signs of cos and sin, bit 29 = swap, bits 28..8 = theta in
+// [0, pi/4) as quarter turns r = u * 2^-22 for the sincos2pi polynomials. No range reduction and no
+// quadrant rotation: two sign-bit inserts and one conditional swap.
+__device__ __forceinline__ void disk_dir(uint32_t ra, float& c_out, float& s_out) {
+  const float r = (float)__builtin_amdgcn_ubfe(ra, 8, 21) * 0x1p-22f;
+  const float r2 = r * r;
+  float ps = fmaf(r2, 0.000160441184787359821f, -0.00468175413531868810f);
+  float pc = fmaf(r2, 0.000919260274839426030f, -0.0208634807633529609f);
+  ps = fmaf(r2, ps, 0.0796926262461670451f);
+  ps = fmaf(r2, ps, -0.645964097506246254f);
+  ps = fmaf(r2, ps, 1.57079632679489662f);
+  const float sn = r * ps;
+  pc = fmaf(r2, pc, 0.253669507901048014f);
+  pc = fmaf(r2, pc, -1.23370055013616983f);
+  const float cs = fmaf(r2, pc, 1.0f);
+  const bool sw = (ra & 0x20000000u) != 0u;
+  const float c = sw ? sn : cs, s = sw ? cs : sn;
+  c_out = __uint_as_float(__float_as_uint(c) ^ (ra & 0x80000000u));
+  s_out = __uint_as_float(__float_as_uint(s) ^ ((ra << 1) & 0x80000000u));
+}
+
 // random_scattering :337-347 (cosine-weighted hemisphere about nl), before the final normalize
 // (the kernel shares that normalize with the camera ray, :536). AXIS: nl is known to be
 // axis-aligned (rect-only scenes); otherwise it is tested per lane, as the oracle does.
@@ -114,9 +136,9 @@ __device__ __forceinline__ void sincos2pi(float xi, float& s_out, float& c_out) 
 // normal component 1-r2 (SPT_FLAG_UNIFORM_SCATTER; oracle c_cosine).
 template <bool AXIS = false>
 __device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool uniform = false) {
-  const float xi1 = u01(ra), xi2 = u01(rb);
+  const float xi2 = u01(rb);
   float s, c;
-  sincos2pi(xi1, s, c);
+  disk_dir(ra, c, s);  // the azimuth r1 = 2*pi*xi1 of :343
   float r2s, s1;
   if (uniform) {
     const float m = xi2 * (2.0f - xi2);

@@ -215,8 +215,10 @@ __device__ __forceinline__ void rect_test(GP g, const Ray6& r, uint64_t up, uint
     n = sel_f(sel1, n0, n1);
   }
   const float tt = n * r.ia;
-  const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
-  const bool inb = (bool)((int)(fabsf(a - g->ma) <= g->ha) & (int)(fabsf(b - g->mb) <= g->hb));
+  // in-plane offsets from the centre, a = d_b * t + (o_b - mid_b): the origin's offset is per ray
+  // and shared by every rectangle with that centre (CSE'd across the unrolled tests)
+  const float a = fmaf(r.db, tt, r.ob - g->ma), b = fmaf(r.dc, tt, r.oc - g->mb);
+  const bool inb = (bool)((int)(fabsf(a) <= g->ha) & (int)(fabsf(b) <= g->hb));
   const uint32_t kk = tkey(tt);
   const bool acc = inb & (kk < tmin_key);
   tmin_key = acc ? kk : tmin_key;
@@ -268,8 +270,8 @@ struct RectHit { float tt; bool inb; };
 template <class GP>
 __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   const float tt = (g->k - r.oa) * r.ia;
-  const float a = fmaf(r.db, tt, r.ob), b = fmaf(r.dc, tt, r.oc);
-  const bool ia = fabsf(a - g->ma) <= g->ha, ib = fabsf(b - g->mb) <= g->hb;
+  const float a = fmaf(r.db, tt, r.ob - g->ma), b = fmaf(r.dc, tt, r.oc - g->mb);
+  const bool ia = fabsf(a) <= g->ha, ib = fabsf(b) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib)};
 }
 
@@ -376,6 +378,11 @@ constexpr int kRegions = 10;
 // by construction.
 __device__ __forceinline__ float hit_plane_t(float n, float da, float ia, float t) {
   return fmaf(fmaf(-t, da, n), ia, t);
+}
+// n / d of the contract (oracle c_div): q = n * rcp_nr(d), one Markstein correction.
+__device__ __forceinline__ float div_mk(float n, float d) {
+  const float y = rcp_nr(d), q = n * y;
+  return fmaf(fmaf(-q, d, n), y, q);
 }
 
 __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
@@ -580,7 +587,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         if (id == D->light_id) {
           SPT_REGION(7);
           e_hit = true;
-          const float pdf = fabsf((D->larea * d.y) / (t * t));           // :471
+          const float pdf = fabsf(div_mk(D->larea * d.y, t * t));        // :471
           const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
           const float w = pdf * brdf;
           T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex

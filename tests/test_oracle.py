@@ -100,6 +100,30 @@ def test_sincos_polynomial_accuracy(oracle):
     assert err < 3e-7
 
 
+def test_disk_dir_octant_mapping(oracle):
+    """The contract's azimuth (spt_oracle_disk_dir): (cos, sin) of the angle the word's bits name —
+    octant by bits 31..29, theta = u * (pi/2) * 2^-22 from bits 28..8 — within 3e-7, unit length,
+    and every octant equally often."""
+    rng = np.random.default_rng(5)
+    words = np.concatenate([rng.integers(0, 1 << 32, 20000, dtype=np.uint64),
+                            [0, 0xFFFFFFFF, 0x1FFFFF00, 0x20000000, 0xE0000000]]).astype(np.uint64)
+    err = 0.0
+    for w in words:
+        w = int(w)
+        th = ((w >> 8) & 0x1FFFFF) * (math.pi / 2) * 2.0 ** -22
+        c, s = math.cos(th), math.sin(th)
+        if w & 0x20000000:
+            c, s = s, c
+        c = -c if w & 0x80000000 else c
+        s = -s if w & 0x40000000 else s
+        gc, gs = oracle.disk_dir(w)
+        err = max(err, abs(gc - c), abs(gs - s), abs(gc * gc + gs * gs - 1.0))
+    assert err < 3e-7
+    phi = np.array([math.atan2(*oracle.disk_dir(int(w))[::-1]) for w in words[:20000]])
+    counts = np.histogram(np.mod(phi, 2 * math.pi), bins=8, range=(0, 2 * math.pi))[0]
+    assert counts.min() > 2300 and counts.max() < 2700, counts
+
+
 def test_rect_intersect_kats(oracle, spt):
     """Ray-rect cases of :102-112 incl. the no-epsilon self-hit and the float in-plane rounding."""
     light = oracle.scene_cornell()[6]  # Rectangle_xz(32,68,63,96,81.5)
