@@ -33,7 +33,7 @@ typedef enum spt_status {
   SPT_ERR_HIP = 2,         /* a HIP runtime call failed (spt_last_error() has the text) */
   SPT_ERR_NO_DEVICE = 3,   /* no usable gfx950 device */
   SPT_ERR_OOM = 4,         /* device allocation failed */
-  SPT_ERR_UNSUPPORTED = 5  /* feature not implemented (e.g. SPEC/REFR material) */
+  SPT_ERR_UNSUPPORTED = 5  /* reserved: feature not implemented (not returned today) */
 } spt_status;
 
 /* Primitive kinds: the reference's Hitable subclasses (:92-254). */

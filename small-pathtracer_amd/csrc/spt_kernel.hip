@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -149,13 +150,17 @@ using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 //   BLACK: 1 = the light's colour is 0, so a path reaching it ends there (RR with p == 0, :448)
 //   MAXD0: 1 = no hard depth cap (max_depth == 0, the reference)
 //   NOS1:  1 = no vertex-1 stream-1 draws (rr_depth >= 1 and nee_prob is 0 or 1)
-template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_>
+//   CAMAX: 1 = axis-aligned camera (horizontal = (h,0,0), vertical = (0,v,0) up to the sign of
+//          zero, origin components nonzero, as the reference's :521 camera): the zero products of
+//          the camera's fma chain vanish exactly, so the ray is the same bits with 5 fewer VALU
+template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_, int CAMAX_>
 struct Cfg {
   static constexpr int NEE = NEE_, LMODE = LMODE_, BLACK = BLACK_, MAXD0 = MAXD0_, NOS1 = NOS1_;
+  static constexpr int CAMAX = CAMAX_;
 };
-using CfgRuntime = Cfg<-1, -1, -1, -1, -1>;
-using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
-using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1>;  // C2: cosine-weighted only
+using CfgRuntime = Cfg<-1, -1, -1, -1, -1, -1>;
+using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
+using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1>;  // C2: cosine-weighted only
 template <class TP>
 __device__ __forceinline__ auto rects_of(const SPT_CONST SceneGeo* G) {
   if constexpr (TP::CONSTGEO) return CornellRectPtr{0};
@@ -456,7 +461,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   bool exhausted = false, capped = false;
   // Wave-uniform event counters (SGPRs), fed by ballots at convergent points of the loop: per-lane
   // counters incremented inside the divergent blocks cost ~40 VGPRs of copies.
-  uint32_t n_path = 0, n_shadow = 0, n_vert = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
+  // (vertices = path rays + NEE light hits: every path ray shades a vertex, hit or miss, and a
+  // shadow ray that reaches the light shades the light's)
+  uint32_t n_path = 0, n_shadow = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
   uint32_t reg_flags = 0;
@@ -523,7 +530,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     if (__ballot(has_unit) == 0) break;
     n_cos += (uint32_t)__popcll(__ballot(gen && cont && !(TP::MAT && spec)));
     // per-lane events of this iteration, counted by ballot at its end
-    bool e_vert = false, e_miss = false, e_nee = false, e_hit = false;
+    bool e_miss = false, e_nee = false, e_hit = false;
 
     // 3) generate the path ray: the cosine continuation from the last vertex (random_scattering
     //    :337-347, its xi from that vertex's Philox words) or the camera ray of a new sample
@@ -551,9 +558,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const float su = (fx + u16(r.x, r.y)) * C->inv_w;
         const float sv = (fy + u16(r.z, r.w)) * C->inv_h;
         o = mk(C->cam[0], C->cam[1], C->cam[2]);
-        v = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
-               fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
-               fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
+        if constexpr (CF::CAMAX == 1) {  // fma(+-0, s, a) == a for a != 0; a == +-0 only meets - o
+          v = mk(fmaf(C->cam[6], su, C->cam[3]) - C->cam[0], fmaf(C->cam[10], sv, C->cam[4]) - C->cam[1],
+                 C->cam[5] - C->cam[2]);
+        } else {
+          v = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
+                 fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
+                 fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
+        }
         T = mk(1, 1, 1);
         L = mk(0, 0, 0);
         depth = 0;
@@ -607,7 +619,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       // 6) shade a vertex (:422, :444-480).
       if (vertex) {
         SPT_REGION(5);
-        e_vert = true;
         const DevPrim& H = s_prims[id];
         const int kind = H.kind;
         f3 x;
@@ -798,7 +809,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         if (TP::MAT) branch = 0;
       }
     }
-    n_vert += (uint32_t)__popcll(__ballot(e_vert));
     n_miss += (uint32_t)__popcll(__ballot(e_miss));
     n_shadow += (uint32_t)__popcll(__ballot(e_nee));
     n_nee_hit += (uint32_t)__popcll(__ballot(e_hit));
@@ -826,7 +836,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       if (capped) atomicAdd(st + 0, 1ull);  // the host reports an error
       atomicAdd(st + 1, (unsigned long long)n_path);
       atomicAdd(st + 2, (unsigned long long)n_shadow);
-      atomicAdd(st + 3, (unsigned long long)n_vert);
+      atomicAdd(st + 3, (unsigned long long)n_path + (unsigned long long)n_nee_hit);
       atomicAdd(st + 4, (unsigned long long)n_shadow);
       atomicAdd(st + 5, (unsigned long long)n_nee_hit);
       atomicAdd(st + 6, (unsigned long long)n_cos);
@@ -1224,8 +1234,12 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                        g.n_txy == 3 && g.n_txz == 4 && g.n_tyz == 3;
   const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
   // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
+  // axis-aligned camera (Cfg CAMAX): horizontal.y/z and vertical.x/z zero, origin nonzero
+  bool cam_axis = K.cam[7] == 0.0f && K.cam[8] == 0.0f && K.cam[9] == 0.0f && K.cam[11] == 0.0f &&
+                  K.cam[0] != 0.0f && K.cam[1] != 0.0f && K.cam[2] != 0.0f;
+  for (int i = 0; i < 12; ++i) cam_axis = cam_axis && std::isfinite(K.cam[i]);
   const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
-                        p->rr_depth >= 1;
+                        p->rr_depth >= 1 && cam_axis;
   int kv = KV_GENERIC;
   if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
   else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;

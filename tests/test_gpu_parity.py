@@ -2,8 +2,9 @@
 counter-mode contract on the same seeded inputs.
 
 Tolerance: the north-star bar is per-channel RMSE < 1e-3 on the linear clamped framebuffer; the
-contract is designed to be BIT-EXACT (explicit fmaf, IEEE div/sqrt, own sincos, integer
-accumulation), so every test below asserts exact equality, which implies the RMSE bar.
+contract is designed to be BIT-EXACT (explicit fmaf, integer-seeded Newton reciprocals with
+Markstein-corrected quotients, own sin/cos polynomials, integer accumulation), so every test
+below asserts exact equality, which implies the RMSE bar.
 """
 import hashlib
 import json
@@ -95,6 +96,18 @@ def test_every_kernel_specialisation_bit_exact(spt, oracle, monkeypatch, kernel,
     gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
     _assert_exact(gpu, cpu)
     assert hashlib.md5(gpu.tobytes()).hexdigest() == GOLD["counter_md5"][est]
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
+@pytest.mark.parametrize("est,q", [("nee", 1.0), ("cos", 0.0)])
+def test_tilted_camera_leaves_the_axis_aligned_specialisation(spt, oracle, est, q):
+    """A camera whose horizontal/vertical vectors are not axis-aligned takes the run-time camera
+    form (Cfg CAMAX only holds for the reference's :521 camera): same contract, same bits."""
+    p = spt.default_params(width=48, height=36, spp=8, seed=17, nee_prob=q)
+    cam = spt.Camera(lookfrom=(40, 55, 160), lookat=(55, 35, 10), vup=(0.1, 1, 0), aspect=48 / 36)
+    gpu, gst = spt.render(spt.cornell_scene(), cam, p, return_stats=True)
+    cpu, cst = oracle.counter_render(spt.cornell_scene(), cam._c, p)
+    _assert_exact(gpu, cpu)
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
