@@ -463,7 +463,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   // counters incremented inside the divergent blocks cost ~40 VGPRs of copies.
   // (vertices = path rays + NEE light hits: every path ray shades a vertex, hit or miss, and a
   // shadow ray that reaches the light shades the light's)
-  uint32_t n_path = 0, n_shadow = 0, n_nee_hit = 0, n_cos = 0, n_miss = 0;
+  uint32_t n_path = 0, n_cos = 0;
+  // Per-lane counts of events that happen inside divergent blocks, incremented in place and
+  // summed once at the end (a boolean per event carried to a convergent ballot cost 3 VALU each).
+  uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
   uint32_t reg_flags = 0;
@@ -530,7 +533,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     if (__ballot(has_unit) == 0) break;
     n_cos += (uint32_t)__popcll(__ballot(gen && cont && !(TP::MAT && spec)));
     // per-lane events of this iteration, counted by ballot at its end
-    bool e_miss = false, e_nee = false, e_hit = false;
 
     // 3) generate the path ray: the cosine continuation from the last vertex (random_scattering
     //    :337-347, its xi from that vertex's Philox words) or the camera ray of a new sample
@@ -598,7 +600,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const SPT_CONST KParams* D = cptr(Pg);
         if (id == D->light_id) {
           SPT_REGION(7);
-          e_hit = true;
+          ++l_hit;
           const float pdf = fabsf(div_mk(D->larea * d.y, t * t));        // :471
           const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
           const float w = pdf * brdf;
@@ -632,14 +634,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
           const float tr = hit_plane_t(H.w1 - oa, da, ia_hit, t);
           x = hit ? mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr) : mk(0, 0, 0);
-          e_miss = !hit;
+          l_miss += hit ? 0u : 1u;
           const float sg = da < 0.0f ? 1.0f : -1.0f;
           nl = mk(kyz ? sg : 0.0f, kxz ? sg : 0.0f, kxy ? sg : 0.0f);
           if (TP::MAT) gn = mk(kyz ? 1.0f : 0.0f, kxz ? 1.0f : 0.0f, kxy ? 1.0f : 0.0f);
         } else {
         if (!hit) {
           x = mk(0, 0, 0);
-          e_miss = true;
+          ++l_miss;
         } else {
           float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
           if (kind == SPT_RECT_XY) tr = hit_plane_t(H.w1 - o.z, d.z, ia_hit, t);
@@ -693,14 +695,18 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           }
         }
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
+        // Every vertex lane takes T*f and moves its origin to x. A lane whose path ends here
+        // restarts at the camera (or pops a REFR child), which resets both; doing it
+        // unconditionally saves the register copies of a conditional update.
+        T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
+        o = x;
+        vid = id;
         if (TP::MAT && !term && H.refl != SPT_DIFF) {
           // SPEC :481-482 and REFR :484-495 (smallpt's commented-out code; oracle c_path): no NEE.
           // reflRay direction r.d - n*2*n.dot(r.d), not renormalised.
-          const f3 Tf = mk(T.x * f.x, T.y * f.y, T.z * f.z);
+          const f3 Tf = T;
           const float k2 = 2.0f * dot3(gn, d);
           const f3 refl = mk(d.x - gn.x * k2, d.y - gn.y * k2, d.z - gn.z * k2);
-          o = x;
-          T = Tf;
           bool use_refl = true;
           if (H.refl == SPT_REFR) {
             const bool into = dot3(gn, nl) > 0.0f;                 // :485
@@ -740,10 +746,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           cont = true;
           spec = true;
         } else if (!term) {
-          // DIFF :457-480. T becomes T*f now; the NEE weight (if the light is reached) multiplies
-          // it when the shadow ray resolves, so T = (T*f)*w exactly as the contract rounds it.
-          T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
-          o = x;
+          // DIFF :457-480. T is T*f now; the NEE weight (if the light is reached) multiplies it
+          // when the shadow ray resolves, so T = (T*f)*w exactly as the contract rounds it.
           const SPT_CONST KParams* D = cptr(Pg);
           bool nee;
           if constexpr (CF::NEE == 1) {
@@ -769,15 +773,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
               zl = fmaf(u01(r.y), D->ldz, D->lz0);
             }
             const f3 dl = normalize3(mk(xl - x.x, D->ly - x.y, zl - x.z));
-            e_nee = true;
+            ++l_nee;
             const SPT_CONST SceneGeo* G2 = cptr(D->geo);
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
             cand = (id == D->light_id) || light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
-            if (cand) {
-              d = dl;
-              vid = id;
-              shadow = true;
-            }
+            d = dl;  // a rejected lane generates its cosine direction next iteration anyway
+            shadow = cand;
           }
           if (!cand) {
             gen = true;
@@ -809,9 +810,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         if (TP::MAT) branch = 0;
       }
     }
-    n_miss += (uint32_t)__popcll(__ballot(e_miss));
-    n_shadow += (uint32_t)__popcll(__ballot(e_nee));
-    n_nee_hit += (uint32_t)__popcll(__ballot(e_hit));
 #ifdef SPT_REGION_STATS
 #pragma unroll
     for (int k = 0; k < kRegions; ++k) {
@@ -835,12 +833,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     if (lane == 0) {  // wave-uniform counters: one lane adds them
       if (capped) atomicAdd(st + 0, 1ull);  // the host reports an error
       atomicAdd(st + 1, (unsigned long long)n_path);
-      atomicAdd(st + 2, (unsigned long long)n_shadow);
-      atomicAdd(st + 3, (unsigned long long)n_path + (unsigned long long)n_nee_hit);
-      atomicAdd(st + 4, (unsigned long long)n_shadow);
-      atomicAdd(st + 5, (unsigned long long)n_nee_hit);
+      atomicAdd(st + 3, (unsigned long long)n_path);  // + the light hits, added per lane below
       atomicAdd(st + 6, (unsigned long long)n_cos);
-      atomicAdd(st + 7, (unsigned long long)n_miss);
+    }
+    {  // per-lane event counts (the atomic optimizer reduces each over the wave)
+      atomicAdd(st + 2, (unsigned long long)l_nee);
+      atomicAdd(st + 3, (unsigned long long)l_hit);
+      atomicAdd(st + 4, (unsigned long long)l_nee);
+      atomicAdd(st + 5, (unsigned long long)l_hit);
+      atomicAdd(st + 7, (unsigned long long)l_miss);
     }
   }
 }
