@@ -315,7 +315,6 @@ def main() -> None:
                                      if traffic else None),
                          "hbm_frac": (round(traffic / (kms.mean() * 1e-3) / 8e12, 5)
                                       if traffic else None),
-                         "frac_vs_nonpacked_78p6": round(achieved / (PEAK_FP32_TFLOPS / 2), 4),
                          "valu_pmc": pmc or None,
                          "kernel": "spt::render_kernel",
                          "kernel_ms": round(float(kms.mean()), 3),
