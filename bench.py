@@ -315,6 +315,10 @@ def main() -> None:
                                      if traffic else None),
                          "hbm_frac": (round(traffic / (kms.mean() * 1e-3) / 8e12, 5)
                                       if traffic else None),
+                         # SURVEY §8(d) asks for both denominators; profiles/r01_valu_rates.txt
+                         # measures v_fma_f32 at full rate and v_pk_fma_f32 at half rate on gfx950,
+                         # so 157.3 (non-packed fma on all lanes) is the binding peak, not 78.6.
+                         "frac_vs_78p6": round(achieved / (PEAK_FP32_TFLOPS / 2), 4),
                          "valu_pmc": pmc or None,
                          "kernel": "spt::render_kernel",
                          "kernel_ms": round(float(kms.mean()), 3),
