@@ -27,15 +27,46 @@ constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
 
 struct u4 { uint32_t x, y, z, w; };
 
+#ifndef SPT_PHILOX_ROUNDS
+#define SPT_PHILOX_ROUNDS 10  // A/B timing builds only: the contract (and the oracle) is 10 rounds
+#endif
 __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
   uint32_t k0 = SPT_PHILOX_KEY0, k1 = SPT_PHILOX_KEY1;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < SPT_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)kPhM0 * c0;  // one v_mad_u64_u32 each (hi and lo together)
     const uint64_t p1 = (uint64_t)kPhM1 * c2;
     const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
     const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
     c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+    k0 += kPhW0; k1 += kPhW1;
+  }
+  return u4{c0, c1, c2, c3};
+}
+
+// The same generator with the counter word c0 (the pixel) and c3 (the seed) fixed for a whole work
+// unit: round 1's product M0 * c0 and its xor with c3 and the first key word are computed once per
+// unit (PxKey), so each call saves one v_mad_u64_u32 and one v_xor. Bit-identical to
+// philox4x32_10(pix, c1, c2, seed).
+struct PxKey { uint32_t hi, lo; };  // hi(M0*pix) ^ seed ^ k1, lo(M0*pix)
+__device__ __forceinline__ PxKey philox_pixel_key(uint32_t pix, uint32_t seed) {
+  const uint64_t p0 = (uint64_t)kPhM0 * pix;
+  return PxKey{(uint32_t)(p0 >> 32) ^ seed ^ (uint32_t)SPT_PHILOX_KEY1, (uint32_t)p0};
+}
+__device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
+  uint32_t k0 = SPT_PHILOX_KEY0, k1 = SPT_PHILOX_KEY1;
+  const uint64_t p1 = (uint64_t)kPhM1 * c2;
+  uint32_t c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, c3 = pk.lo;
+  c1 = (uint32_t)p1;
+  c2 = pk.hi;
+  k0 += kPhW0; k1 += kPhW1;
+#pragma unroll
+  for (int r = 1; r < SPT_PHILOX_ROUNDS; ++r) {
+    const uint64_t p0 = (uint64_t)kPhM0 * c0;
+    const uint64_t q1 = (uint64_t)kPhM1 * c2;
+    const uint32_t n0 = (uint32_t)(q1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0; c1 = (uint32_t)q1; c2 = n2; c3 = (uint32_t)p0;
     k0 += kPhW0; k1 += kPhW1;
   }
   return u4{c0, c1, c2, c3};

@@ -450,7 +450,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   bool spec = false;      // the continuation direction is already set (SPEC/REFR, MAT only)
   uint32_t branch = 0;    // path-tree position of a REFR split (counter word 2 bits 24+; MAT only)
   int sp = 0;             // pending refraction children in s_stack (MAT only)
-  uint32_t lp = 0, s = 0, s_end = 0, pix = 0;
+  uint32_t lp = 0, s = 0, s_end = 0;
+  PxKey pk = PxKey{0, 0};  // Philox round-1 terms of the unit's pixel (philox_pixel_key)
   int depth = 0, vid = 0;
   float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5), (h - y - 1 - 0.5) of :533-534
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
@@ -519,7 +520,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const uint32_t T_ = (uint32_t)Q->tile_rows;
         const uint32_t tile = div_magic(lr, Q->m_tile, Q->sh_tile), within = lr - tile * T_;
         const int py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
-        pix = (uint32_t)py * w + (uint32_t)px;
+        pk = philox_pixel_key((uint32_t)py * w + (uint32_t)px, Q->seed);
         fx = (float)px - 0.5f;
         fy = (float)(Q->height - py - 1) - 0.5f;
         has_unit = true;
@@ -549,9 +550,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         }
       }
       const uint32_t bw = TP::MAT ? branch << 24 : 0u;
-      r = philox4x32_10(pix, s, (cont ? (uint32_t)depth + 1u : 1u) | bw, cptr(Pg)->seed);
+      r = philox_px(pk, s, (cont ? (uint32_t)depth + 1u : 1u) | bw);
       if (SPT_PROBE & 1) {
-        const u4 r2 = philox4x32_10(opq(pix), s, cont ? (uint32_t)depth + 1u : 1u, cptr(Pg)->seed);
+        const u4 r2 = philox_px(PxKey{opq(pk.hi), pk.lo}, s, cont ? (uint32_t)depth + 1u : 1u);
         if (opq(0u) != 0u) r = r2;
       }
       if (!cont) {
@@ -609,7 +610,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
           // random draw; anything else is shaded with that vertex's own Philox words.
           if (CF::BLACK != 1 && !(hit && s_prims[id].pmax == 0.0f))
-            r = philox4x32_10(pix, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u), D->seed);
+            r = philox_px(pk, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u));
           vertex = true;
         } else {
           gen = true;  // occluded: continue with the cosine sample (:468-469), T = T*f
@@ -674,7 +675,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         if (CF::NOS1 != 1 && depth == 1) {
           const SPT_CONST KParams* C = cptr(Pg);
           if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
-            rl = philox4x32_10(pix, s, 1u | 0x80000000u, C->seed);
+            rl = philox_px(pk, s, 1u | 0x80000000u);
         }
         // Russian roulette :448-454 (+ optional hard depth cap).
         const int max_depth = CF::MAXD0 == 1 ? 0 : P->max_depth;
