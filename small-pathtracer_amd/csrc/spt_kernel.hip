@@ -476,6 +476,22 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   for (uint32_t iter = 0;; ++iter) {
     const SPT_CONST KParams* P = cptr(Pg);
     SPT_REGION(0);  // loop iteration
+#if defined(SPT_EXTRA_SALU) || defined(SPT_EXTRA_VALU)
+    {  // marginal-cost probes (A/B builds only): N extra SALU / VALU per iteration, results unused
+#ifdef SPT_EXTRA_SALU
+      uint64_t sd = (uint64_t)iter;
+#pragma unroll
+      for (int q = 0; q < SPT_EXTRA_SALU; ++q) asm volatile("s_and_b64 %0, %0, %0" : "+s"(sd) :: "scc");
+      asm volatile("" ::"s"(sd));
+#endif
+#ifdef SPT_EXTRA_VALU
+      float dv = fx;
+#pragma unroll
+      for (int q = 0; q < SPT_EXTRA_VALU; ++q) asm volatile("v_fma_f32 %0, %0, %0, %0" : "+v"(dv));
+      asm volatile("" ::"v"(dv));
+#endif
+    }
+#endif
     if (iter >= kMaxWaveIters) {  // runaway guard: drop the work, leave through the normal exit
       capped = true;                // (a second loop exit would duplicate the loop state)
       exhausted = true;
