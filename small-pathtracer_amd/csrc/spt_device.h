@@ -107,8 +107,8 @@ __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a
 // Vec::norm :50-52 as *this * rsq(len2); exactly-unit vectors are returned unchanged.
 __device__ __forceinline__ f3 normalize3(f3 v) {
   const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
-  if (l2 == 1.0f) return v;
-  const float inv = rsq_nr(l2);
+  // exactly-unit vectors come back unchanged as v * 1 (exact): a select, not a branch
+  const float inv = l2 == 1.0f ? 1.0f : rsq_nr(l2);
   return mk(v.x * inv, v.y * inv, v.z * inv);
 }
 // operator% :56-58

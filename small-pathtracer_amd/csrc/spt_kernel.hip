@@ -36,6 +36,14 @@ constexpr int kMaxPrims = 64;
 constexpr int kBlock = 256;
 constexpr uint32_t kGrab = 64;  // units fetched per queue atomic
 constexpr int kStatWords = 32;
+// Lane states of the render loop (render_kernel).
+constexpr uint32_t kStIdle = 0;    // no work unit
+constexpr uint32_t kStCam = 1;     // next: a camera ray (a new sample; retire the unit at s_end)
+constexpr uint32_t kStCos = 2;     // next: the cosine continuation of the last vertex
+constexpr uint32_t kStSpec = 3;    // next: a path ray whose direction is already set (SPEC/REFR)
+constexpr uint32_t kStPath = 4;    // a path ray is set: trace it, shade its vertex
+constexpr uint32_t kStShadow = 5;  // a NEE shadow ray toward the light is set: trace, resolve
+constexpr uint32_t kStTerm = 6;    // the path ended at this vertex (within an iteration)
 // Exit condition every wave reaches even if a path never terminated: a C3 wave runs ~4e3
 // iterations and a 1-GPU C5 wave ~3e6; stats[0] counts waves that hit the cap.
 constexpr uint32_t kMaxWaveIters = 1u << 26;  // [0,8) path stats, [8,28) region stats (diagnostic build)
@@ -216,7 +224,10 @@ __device__ __forceinline__ void rect_test(GP g, const Ray6& r, uint64_t up, uint
   uint64_t sel1 = 0;
   if constexpr (PAIR) {
     const float n1 = g->k1 - r.oa;
-    sel1 = (up & ~lanes(n0 > 0.0f)) | (~up & lanes(n1 < 0.0f));
+    // sel1 = up ? !(n0 > 0) : (n1 < 0) (oracle c_intersect) as ONE compare and one SALU xor:
+    // z = up ? n0 : -n1, sel1 = (z > 0) ^ up -- exact for every n0, n1 (NaN and signed zeros incl.)
+    const float z = (r.ia > 0.0f) ? n0 : -n1;
+    sel1 = lanes(z > 0.0f) ^ up;
     n = sel_f(sel1, n0, n1);
   }
   const float tt = n * r.ia;
@@ -443,16 +454,17 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
 
   const uint32_t lane = __lane_id();
   // ---- per-lane state
-  bool has_unit = false;  // owns a work unit (pixel, sample range)
-  bool gen = false;       // needs a new path ray: camera (cont == false) or cosine continuation
-  bool cont = false;
-  bool shadow = false;    // the pending ray is a NEE shadow ray from vertex o
-  bool spec = false;      // the continuation direction is already set (SPEC/REFR, MAT only)
+  // The lane's state is ONE integer in a VGPR (kSt*), not a set of booleans: LLVM keeps loop-carried
+  // booleans as 64-bit lane masks and merges each one at every join of the divergent blocks with an
+  // s_andn2/s_and/s_or triple, and SALU issue bounds this loop (one scalar unit per CU; a marginal
+  // SALU instruction costs ~3x a marginal VALU one here). A VGPR state is
+  // written under exec and needs no merge.
+  uint32_t ls = kStIdle;
   uint32_t branch = 0;    // path-tree position of a REFR split (counter word 2 bits 24+; MAT only)
   int sp = 0;             // pending refraction children in s_stack (MAT only)
   uint32_t lp = 0, s = 0, s_end = 0;
   PxKey pk = PxKey{0, 0};  // Philox round-1 terms of the unit's pixel (philox_pixel_key)
-  int depth = 0, vid = 0;
+  int depth = 0, vid = 0;  // depth: vertices of the current path so far (0 until its first)
   float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5), (h - y - 1 - 0.5) of :533-534
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
   f3 o = mk(0, 0, 0), d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
@@ -495,21 +507,20 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     if (iter >= kMaxWaveIters) {  // runaway guard: drop the work, leave through the normal exit
       capped = true;                // (a second loop exit would duplicate the loop state)
       exhausted = true;
-      has_unit = false;
+      ls = kStIdle;
     }
     // 1) retire finished units: flush the fixed-point sums of their pixel.
-    if (has_unit && gen && !cont && s >= s_end) {
+    if (ls == kStCam && s >= s_end) {
       SPT_REGION(1);
       unsigned long long* a = P->accum + 3ull * lp;
       if (acc0) atomicAdd(a + 0, acc0);
       if (acc1) atomicAdd(a + 1, acc1);
       if (acc2) atomicAdd(a + 2, acc2);
       acc0 = acc1 = acc2 = 0;
-      has_unit = false;
-      gen = false;
+      ls = kStIdle;
     }
     // 2) refill idle lanes from the wave's pool (ballot + mbcnt prefix sum), pool from the queue.
-    bool needs_unit = !has_unit;
+    bool needs_unit = ls == kStIdle;
     uint64_t need = __ballot(needs_unit);
     while (need != 0 && !exhausted) {
       SPT_REGION(2);
@@ -539,68 +550,68 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         pk = philox_pixel_key((uint32_t)py * w + (uint32_t)px, Q->seed);
         fx = (float)px - 0.5f;
         fy = (float)(Q->height - py - 1) - 0.5f;
-        has_unit = true;
+        ls = kStCam;
         needs_unit = false;
-        gen = true;
-        cont = false;
       }
       pool_next += min((uint32_t)__popcll(need), avail);
       need = __ballot(needs_unit);
     }
-    if (__ballot(has_unit) == 0) break;
-    n_cos += (uint32_t)__popcll(__ballot(gen && cont && !(TP::MAT && spec)));
-    // per-lane events of this iteration, counted by ballot at its end
+    if (__ballot(ls != kStIdle) == 0) break;
+    n_cos += (uint32_t)__popcll(__ballot(ls == kStCos));
 
-    // 3) generate the path ray: the cosine continuation from the last vertex (random_scattering
-    //    :337-347, its xi from that vertex's Philox words) or the camera ray of a new sample
-    //    (:533-536, jitter from the low bytes of vertex 1's words), one Philox call for the
-    //    vertex the ray leads to, one normalize for both.
-    if (gen) {
-      f3 v = mk(0, 0, 0);
-      if (cont && !(TP::MAT && spec)) {
-        SPT_REGION(8);
-        v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
-        if (SPT_PROBE & 8) {
-          const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
-          if (opq(0u) != 0u) v = v2;
-        }
+    // 3) generate the path ray (kStCam, kStCos, kStSpec): the cosine continuation from the last
+    //    vertex (random_scattering :337-347, its xi from that vertex's Philox words) or the camera
+    //    ray of a new sample (:533-536, jitter from the low bytes of vertex 1's words), one Philox
+    //    call for the vertex the ray leads to, one normalize for both. Both directions are computed
+    //    for every generating lane and selected: a wave nearly always holds lanes of both kinds, so
+    //    branches would save no VALU and cost their exec-mask SALU.
+    if (ls - kStCam < 3u) {
+      const bool cam = ls == kStCam;
+      if (ls != kStSpec) SPT_REGION(cam ? 3 : 8);
+      f3 v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
+      if (SPT_PROBE & 8) {
+        const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
+        if (opq(0u) != 0u) v = v2;
       }
-      const uint32_t bw = TP::MAT ? branch << 24 : 0u;
-      r = philox_px(pk, s, (cont ? (uint32_t)depth + 1u : 1u) | bw);
+      // the vertex this ray leads to: depth + 1 (depth == 0 for a new sample's camera ray)
+      const uint32_t ctr2 = ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u);
+      r = philox_px(pk, s, ctr2);
       if (SPT_PROBE & 1) {
-        const u4 r2 = philox_px(PxKey{opq(pk.hi), pk.lo}, s, cont ? (uint32_t)depth + 1u : 1u);
+        const u4 r2 = philox_px(PxKey{opq(pk.hi), pk.lo}, s, ctr2);
         if (opq(0u) != 0u) r = r2;
       }
-      if (!cont) {
-        SPT_REGION(3);
+      {
         const SPT_CONST KParams* C = cptr(Pg);
         const float su = (fx + u16(r.x, r.y)) * C->inv_w;
         const float sv = (fy + u16(r.z, r.w)) * C->inv_h;
-        o = mk(C->cam[0], C->cam[1], C->cam[2]);
+        f3 vc;
         if constexpr (CF::CAMAX == 1) {  // fma(+-0, s, a) == a for a != 0; a == +-0 only meets - o
-          v = mk(fmaf(C->cam[6], su, C->cam[3]) - C->cam[0], fmaf(C->cam[10], sv, C->cam[4]) - C->cam[1],
-                 C->cam[5] - C->cam[2]);
+          vc = mk(fmaf(C->cam[6], su, C->cam[3]) - C->cam[0], fmaf(C->cam[10], sv, C->cam[4]) - C->cam[1],
+                  C->cam[5] - C->cam[2]);
         } else {
-          v = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
-                 fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
-                 fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
+          vc = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
+                  fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
+                  fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
         }
-        T = mk(1, 1, 1);
-        L = mk(0, 0, 0);
-        depth = 0;
+        v = mk(cam ? vc.x : v.x, cam ? vc.y : v.y, cam ? vc.z : v.z);
+        o = mk(cam ? C->cam[0] : o.x, cam ? C->cam[1] : o.y, cam ? C->cam[2] : o.z);
       }
-      if (!(TP::MAT && spec)) d = normalize3(v);
-      shadow = false;
-      gen = false;
-      spec = false;
+      const f3 dn = normalize3(v);
+      if constexpr (TP::MAT) {  // a SPEC/REFR direction is set already
+        const bool keep = ls == kStSpec;
+        d = mk(keep ? d.x : dn.x, keep ? d.y : dn.y, keep ? d.z : dn.z);
+      } else {
+        d = dn;
+      }
+      ls = kStPath;
     }
 
-    n_path += (uint32_t)__popcll(__ballot(has_unit && !shadow));
-    if (has_unit) {
+    n_path += (uint32_t)__popcll(__ballot(ls == kStPath));
+    if (ls >= kStPath) {  // kStPath or kStShadow
       // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
       SPT_REGION(4);
       const SPT_CONST SceneGeo* G = cptr(P->geo);
-      int id = shadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
+      int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
       float t, ia_hit;
       bool hit = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, o, d, t, id, ia_hit);
       if (SPT_PROBE & 2) {
@@ -609,34 +620,30 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2, ia2);
         if (opq(0u) != 0u) { hit = h2; t = t2; id = id2; ia_hit = ia2; }
       }
-      bool vertex = !shadow, term = false;
 
-      // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467).
-      if (shadow) {
+      // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467). Then
+      //    the light is the next vertex (shaded in the common block below, T = T*f*weight); else the
+      //    cosine sample follows (:468-469, T = T*f). The weight is computed for every shadow lane
+      //    and applied as T*1 (exact) where the light is not reached: no branch.
+      if (ls == kStShadow) {
         SPT_REGION(6);
         const SPT_CONST KParams* D = cptr(Pg);
-        if (id == D->light_id) {
-          SPT_REGION(7);
-          ++l_hit;
-          const float pdf = fabsf(div_mk(D->larea * d.y, t * t));        // :471
-          const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
-          const float w = pdf * brdf;
-          T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
-          // The light hit by this very ray is the next vertex, shaded in the common block below.
-          // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
-          // random draw; anything else is shaded with that vertex's own Philox words.
-          if (CF::BLACK != 1 && !(hit && s_prims[id].pmax == 0.0f))
-            r = philox_px(pk, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u));
-          vertex = true;
-        } else {
-          gen = true;  // occluded: continue with the cosine sample (:468-469), T = T*f
-          cont = true;
-        }
-        shadow = false;
+        const bool lh = id == D->light_id;
+        if (lh) SPT_REGION(7);
+        l_hit += lh ? 1u : 0u;
+        const float pdf = fabsf(div_mk(D->larea * d.y, t * t));        // :471
+        const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
+        const float w = lh ? pdf * brdf : 1.0f;
+        T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
+        // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
+        // random draw; anything else is shaded with that vertex's own Philox words.
+        if (CF::BLACK != 1 && lh && !(hit && s_prims[id].pmax == 0.0f))
+          r = philox_px(pk, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u));
+        ls = lh ? kStPath : kStCos;
       }
 
       // 6) shade a vertex (:422, :444-480).
-      if (vertex) {
+      if (ls == kStPath) {
         SPT_REGION(5);
         const DevPrim& H = s_prims[id];
         const int kind = H.kind;
@@ -693,24 +700,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           if (C->rr_depth < 1 || (C->nee_prob > 0.0f && C->nee_prob < 1.0f))
             rl = philox_px(pk, s, 1u | 0x80000000u);
         }
-        // Russian roulette :448-454 (+ optional hard depth cap).
+        // Russian roulette :448-454 (+ optional hard depth cap), branch-free: f is scaled by the
+        // host-rounded 1/p wherever RR applies (f * 1 elsewhere, exact); f is unused on a path that
+        // ends here.
         const int max_depth = CF::MAXD0 == 1 ? 0 : P->max_depth;
-        if (max_depth > 0 && depth >= max_depth) {
-          term = true;
-        } else if (depth > P->rr_depth || p == 0.0f) {
-          if (!(p > 0.0f)) {
-            term = true;
-          } else {
-            bool keep = true;
-            if (p < 1.0f) keep = u16(rl.x, rl.y) < p;
-            if (keep) {
-              const float ip = H.ip;  // == 1.0f / p
-              f = mk(f.x * ip, f.y * ip, f.z * ip);
-            } else {
-              term = true;
-            }
-          }
-        }
+        const bool capd = (max_depth > 0) & (depth >= max_depth);
+        const bool rr = (depth > P->rr_depth) | (p == 0.0f);
+        const bool keep = (p > 0.0f) & ((!(p < 1.0f)) | (u16(rl.x, rl.y) < p));
+        const bool term = capd | (rr & !keep);
+        const float fsc = rr ? H.ip : 1.0f;  // H.ip == 1.0f / p
+        f = mk(f.x * fsc, f.y * fsc, f.z * fsc);
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
         // Every vertex lane takes T*f and moves its origin to x. A lane whose path ends here
         // restarts at the camera (or pops a REFR child), which resets both; doing it
@@ -718,6 +717,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
         o = x;
         vid = id;
+        uint32_t nxt = kStCos;  // the state after this vertex unless the path ends here
         if (TP::MAT && !term && H.refl != SPT_DIFF) {
           // SPEC :481-482 and REFR :484-495 (smallpt's commented-out code; oracle c_path): no NEE.
           // reflRay direction r.d - n*2*n.dot(r.d), not renormalised.
@@ -759,12 +759,11 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
             }
           }
           if (use_refl) d = refl;
-          gen = true;
-          cont = true;
-          spec = true;
-        } else if (!term) {
+          nxt = kStSpec;
+        } else {
           // DIFF :457-480. T is T*f now; the NEE weight (if the light is reached) multiplies it
           // when the shadow ray resolves, so T = (T*f)*w exactly as the contract rounds it.
+          // Computed for every vertex lane (a lane whose path ends here discards it): no branch.
           const SPT_CONST KParams* D = cptr(Pg);
           bool nee;
           if constexpr (CF::NEE == 1) {
@@ -777,7 +776,6 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
             else if (q <= 0.0f) nee = false;
             else nee = u16(rl.z, rl.w) < q;
           }
-          bool cand = false;
           if (nee) {
             // light_sampling :363-369 and the shadow-ray direction :466.
             float xl, zl;
@@ -790,41 +788,41 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
               zl = fmaf(u01(r.y), D->ldz, D->lz0);
             }
             const f3 dl = normalize3(mk(xl - x.x, D->ly - x.y, zl - x.z));
-            ++l_nee;
+            l_nee += term ? 0u : 1u;
             const SPT_CONST SceneGeo* G2 = cptr(D->geo);
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
-            cand = (id == D->light_id) || light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
+            const bool la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
+            const bool cand = (id == D->light_id) | la;
             d = dl;  // a rejected lane generates its cosine direction next iteration anyway
-            shadow = cand;
-          }
-          if (!cand) {
-            gen = true;
-            cont = true;
+            nxt = cand ? kStShadow : kStCos;
           }
         }
+        ls = term ? kStTerm : nxt;
       }
       // 7) path end: accumulate this sample (:536-538) and start the next one.
-      if (TP::MAT && term && sp > 0) {  // the pending refraction child of a REFR split
-        --sp;
-        const Node& N = s_stack[threadIdx.x * 2 + sp];
-        o = mk(N.o[0], N.o[1], N.o[2]);
-        d = mk(N.d[0], N.d[1], N.d[2]);
-        T = mk(N.T[0], N.T[1], N.T[2]);
-        depth = N.depth;
-        branch = N.branch;
-        gen = true;
-        cont = true;
-        spec = true;
-      } else if (term) {
-        SPT_REGION(9);
-        const float scale = cptr(Pg)->fix_scale;
-        acc0 += fix31(L.x, scale);
-        acc1 += fix31(L.y, scale);
-        acc2 += fix31(L.z, scale);
-        ++s;
-        gen = true;
-        cont = false;
-        if (TP::MAT) branch = 0;
+      if (ls == kStTerm) {
+        if (TP::MAT && sp > 0) {  // the pending refraction child of a REFR split
+          --sp;
+          const Node& N = s_stack[threadIdx.x * 2 + sp];
+          o = mk(N.o[0], N.o[1], N.o[2]);
+          d = mk(N.d[0], N.d[1], N.d[2]);
+          T = mk(N.T[0], N.T[1], N.T[2]);
+          depth = N.depth;
+          branch = N.branch;
+          ls = kStSpec;
+        } else {
+          SPT_REGION(9);
+          const float scale = cptr(Pg)->fix_scale;
+          acc0 += fix31(L.x, scale);
+          acc1 += fix31(L.y, scale);
+          acc2 += fix31(L.z, scale);
+          ++s;
+          L = mk(0, 0, 0);
+          T = mk(1, 1, 1);
+          depth = 0;
+          if (TP::MAT) branch = 0;
+          ls = kStCam;
+        }
       }
     }
 #ifdef SPT_REGION_STATS
