@@ -101,6 +101,14 @@ __device__ __forceinline__ float rsq_nr(float x) {
   return y;
 }
 
+// Materialise v here, unconditionally: LLVM turns `c ? a : expensive(b)` back into a branch around
+// the expensive side, and each such branch costs exec-mask SALU, the loop's binding resource.
+template <typename T>
+__device__ __forceinline__ T keep(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
@@ -108,7 +116,8 @@ __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a
 __device__ __forceinline__ f3 normalize3(f3 v) {
   const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
   // exactly-unit vectors come back unchanged as v * 1 (exact): a select, not a branch
-  const float inv = l2 == 1.0f ? 1.0f : rsq_nr(l2);
+  const float rs = keep(rsq_nr(l2));
+  const float inv = l2 == 1.0f ? 1.0f : rs;
   return mk(v.x * inv, v.y * inv, v.z * inv);
 }
 // operator% :56-58

@@ -341,7 +341,8 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   const int nxy = TP::CONSTGEO ? kCornellNXY : n_of<TP>(TP::NXY, G->n_xy);
   const int nxz = TP::CONSTGEO ? kCornellNXZ : n_of<TP>(TP::NXZ, G->n_xz);
   ia_hit = pos < nxy ? iz : (pos < nxy + nxz ? iy : ix);
-  if (pos >= 0) id = pos2idx[pos];
+  const int idn = keep(pos2idx[pos < 0 ? 0 : pos]);  // (unconditional LDS read: no branch)
+  id = pos >= 0 ? idn : id;
   return tmin < 1e20f;
 }
 
@@ -657,7 +658,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
           const float tr = hit_plane_t(H.w1 - oa, da, ia_hit, t);
-          x = hit ? mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr) : mk(0, 0, 0);
+          x = mk(keep(o.x + d.x * tr), keep(o.y + d.y * tr), keep(o.z + d.z * tr));
+          x = hit ? x : mk(0, 0, 0);  // a miss vertex is the origin (:373-374)
           l_miss += hit ? 0u : 1u;
           const float sg = da < 0.0f ? 1.0f : -1.0f;
           nl = mk(kyz ? sg : 0.0f, kxz ? sg : 0.0f, kxy ? sg : 0.0f);
