@@ -468,7 +468,9 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   int depth = 0, vid = 0;  // depth: vertices of the current path so far (0 until its first)
   float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5), (h - y - 1 - 0.5) of :533-534
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
-  f3 o = mk(0, 0, 0), d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
+  // o starts at the camera (the first ray of every sample is a camera ray; the path end resets it)
+  f3 o = mk(cptr(Pg)->cam[0], cptr(Pg)->cam[1], cptr(Pg)->cam[2]);
+  f3 d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
   u4 r = u4{0, 0, 0, 0};  // Philox words of the vertex the pending path ray leads to
   // ---- wave-uniform state
   uint32_t pool_next = 0, pool_end = 0;
@@ -594,20 +596,21 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
                   fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
                   fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
         }
-        v = mk(cam ? vc.x : v.x, cam ? vc.y : v.y, cam ? vc.z : v.z);
-        o = mk(cam ? C->cam[0] : o.x, cam ? C->cam[1] : o.y, cam ? C->cam[2] : o.z);
+        v = mk(cam ? vc.x : v.x, cam ? vc.y : v.y, cam ? vc.z : v.z);  // o: set at the path end
       }
       const f3 dn = normalize3(v);
       if constexpr (TP::MAT) {  // a SPEC/REFR direction is set already
-        const bool keep = ls == kStSpec;
-        d = mk(keep ? d.x : dn.x, keep ? d.y : dn.y, keep ? d.z : dn.z);
+        const bool kd = ls == kStSpec;
+        d = mk(kd ? d.x : dn.x, kd ? d.y : dn.y, kd ? d.z : dn.z);
       } else {
         d = dn;
       }
       ls = kStPath;
     }
 
-    n_path += (uint32_t)__popcll(__ballot(ls == kStPath));
+    // Path rays: counted here by the generic kernel only. Without SPEC/REFR every path ray is a
+    // sample's camera ray or a cosine continuation, so the others add n_cos + samples at the end.
+    if constexpr (TP::MAT) n_path += (uint32_t)__popcll(__ballot(ls == kStPath));
     if (ls >= kStPath) {  // kStPath or kStShadow
       // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
       SPT_REGION(4);
@@ -708,9 +711,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const int max_depth = CF::MAXD0 == 1 ? 0 : P->max_depth;
         const bool capd = (max_depth > 0) & (depth >= max_depth);
         const bool rr = (depth > P->rr_depth) | (p == 0.0f);
-        const bool keep = (p > 0.0f) & ((!(p < 1.0f)) | (u16(rl.x, rl.y) < p));
-        const bool term = capd | (rr & !keep);
-        const float fsc = rr ? H.ip : 1.0f;  // H.ip == 1.0f / p
+        const bool alive = (p > 0.0f) & ((!(p < 1.0f)) | (u16(rl.x, rl.y) < p));
+        const bool term = capd | (rr & !alive);
+        const float ip = keep(H.ip);  // == 1.0f / p, read unconditionally (no branch)
+        const float fsc = rr ? ip : 1.0f;
         f = mk(f.x * fsc, f.y * fsc, f.z * fsc);
         L = mk(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
         // Every vertex lane takes T*f and moves its origin to x. A lane whose path ends here
@@ -822,6 +826,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           L = mk(0, 0, 0);
           T = mk(1, 1, 1);
           depth = 0;
+          {
+            const SPT_CONST KParams* C = cptr(Pg);
+            o = mk(C->cam[0], C->cam[1], C->cam[2]);  // the next sample's camera ray
+          }
           if (TP::MAT) branch = 0;
           ls = kStCam;
         }
@@ -849,9 +857,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
 #endif
     if (lane == 0) {  // wave-uniform counters: one lane adds them
       if (capped) atomicAdd(st + 0, 1ull);  // the host reports an error
-      atomicAdd(st + 1, (unsigned long long)n_path);
-      atomicAdd(st + 3, (unsigned long long)n_path);  // + the light hits, added per lane below
+      const unsigned long long np = TP::MAT ? n_path : n_cos;  // (+ samples below, !MAT)
+      atomicAdd(st + 1, np);
+      atomicAdd(st + 3, np);  // + the light hits, added per lane below
       atomicAdd(st + 6, (unsigned long long)n_cos);
+    }
+    if (!TP::MAT && blockIdx.x == 0 && threadIdx.x == 0) {  // one camera ray per sample
+      const SPT_CONST KParams* C = cptr(Pg);
+      const unsigned long long samples = (unsigned long long)C->n_local_pix * (unsigned long long)C->spp;
+      atomicAdd(st + 1, samples);
+      atomicAdd(st + 3, samples);
     }
     {  // per-lane event counts (the atomic optimizer reduces each over the wave)
       atomicAdd(st + 2, (unsigned long long)l_nee);
