@@ -40,6 +40,16 @@ __global__ void __launch_bounds__(256) k_rate(uint32_t* out, uint32_t seed) {
     if constexpr (K == 11) { DO("v_mul_hi_u32_u24") }
     if constexpr (K == 12) { DO1("v_rsq_f32") }
     if constexpr (K == 13) { DO3("v_med3_f32") }
+#define DOB(INS) asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a0) : "v"(b)); asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a1) : "v"(b)); \
+  asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a2) : "v"(b)); asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a3) : "v"(b)); \
+  asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a4) : "v"(b)); asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a5) : "v"(b)); \
+  asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a6) : "v"(b)); asm volatile(INS " %0, %0, %1, %0 bitop3:0x96" : "+v"(a7) : "v"(b));
+    if constexpr (K == 14) { DOB("v_bitop3_b32") }
+    if constexpr (K == 15) { DO1("v_cvt_f32_u32") }
+    if constexpr (K == 16) { DO3("v_add3_u32") }
+    if constexpr (K == 17) { DO3("v_xad_u32") }
+    if constexpr (K == 18) { DO3("v_perm_b32") }
+    if constexpr (K == 19) { DO3("v_lshl_add_u32") }
   }
   out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
@@ -112,7 +122,8 @@ int main() {
   R32(0, "v_add_u32") R32(1, "v_mul_lo_u32") R32(2, "v_mul_hi_u32") R32(3, "v_mul_u32_u24")
   R32(11, "v_mul_hi_u32_u24") R32(4, "v_mul_f32") R32(5, "v_fma_f32") R32(6, "v_sqrt_f32")
   R32(7, "v_rcp_f32") R32(12, "v_rsq_f32") R32(8, "v_sin_f32") R32(9, "v_xor_b32")
-  R32(10, "v_or3_b32") R32(13, "v_med3_f32")
+  R32(10, "v_or3_b32") R32(13, "v_med3_f32") R32(14, "v_bitop3_b32") R32(15, "v_cvt_f32_u32")
+  R32(16, "v_add3_u32") R32(17, "v_xad_u32") R32(18, "v_perm_b32") R32(19, "v_lshl_add_u32")
   R64(0, "v_pk_fma_f32") R64(1, "v_pk_mul_f32") R64(2, "v_pk_add_f32") R64(3, "v_mad_u64_u32")
   R64(4, "v_fma_f64")
   printf("CUs %d clock %d kHz\n", ncu, p.clockRate);
