@@ -53,6 +53,13 @@ __device__ __forceinline__ PxKey philox_pixel_key(uint32_t pix, uint32_t seed) {
   const uint64_t p0 = (uint64_t)kPhM0 * pix;
   return PxKey{(uint32_t)(p0 >> 32) ^ seed ^ (uint32_t)SPT_PHILOX_KEY1, (uint32_t)p0};
 }
+// a ^ b ^ k in ONE full-rate v_bitop3_b32 (tools/valu_rates: v_xor and v_bitop3 issue at the same
+// rate), k a compile-time round key held in an SGPR: halves the xor count of a Philox round.
+__device__ __forceinline__ uint32_t xor3k(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
 __device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
   uint32_t k0 = SPT_PHILOX_KEY0, k1 = SPT_PHILOX_KEY1;
   const uint64_t p1 = (uint64_t)kPhM1 * c2;
@@ -64,8 +71,13 @@ __device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
   for (int r = 1; r < SPT_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)kPhM0 * c0;
     const uint64_t q1 = (uint64_t)kPhM1 * c2;
+#ifdef SPT_PHILOX_XOR2
     const uint32_t n0 = (uint32_t)(q1 >> 32) ^ c1 ^ k0;
     const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+#else
+    const uint32_t n0 = xor3k((uint32_t)(q1 >> 32), c1, k0);
+    const uint32_t n2 = xor3k((uint32_t)(p0 >> 32), c3, k1);
+#endif
     c0 = n0; c1 = (uint32_t)q1; c2 = n2; c3 = (uint32_t)p0;
     k0 += kPhW0; k1 += kPhW1;
   }
