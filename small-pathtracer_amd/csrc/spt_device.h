@@ -87,7 +87,8 @@ __device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
 // 16-bit draw from the low bytes of two Philox words (RR and NEE-mix draws, see the kernel).
 __device__ __forceinline__ float u16(uint32_t lo, uint32_t hi) {
-  return (float)((lo & 0xFFu) | ((hi & 0xFFu) << 8)) * 0x1p-16f;
+  // (lo & 0xFF) | (hi & 0xFF) << 8 as ONE v_perm_b32 (bytes {hi:lo}[4], [0], zero, zero)
+  return (float)__builtin_amdgcn_perm(hi, lo, 0x0C0C0400u) * 0x1p-16f;
 }
 
 // ---- deterministic reciprocal / reciprocal square root (contract): integer seed + 3 Newton
