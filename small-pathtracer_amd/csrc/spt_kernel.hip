@@ -161,14 +161,27 @@ using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 //   CAMAX: 1 = axis-aligned camera (horizontal = (h,0,0), vertical = (0,v,0) up to the sign of
 //          zero, origin components nonzero, as the reference's :521 camera): the zero products of
 //          the camera's fma chain vanish exactly, so the ray is the same bits with 5 fewer VALU
-template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_, int CAMAX_>
+//   LREF:  1 = the reference's light sampling and RR constants (light x0/dx 32/36, z0/dz 63/36,
+//          y 81.6, area 1296 :365-367,:471; light id 6 :467; rr_depth 5 :448): literals instead
+//          of scalar loads in the loop
+template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_, int CAMAX_, int LREF_ = 0>
 struct Cfg {
   static constexpr int NEE = NEE_, LMODE = LMODE_, BLACK = BLACK_, MAXD0 = MAXD0_, NOS1 = NOS1_;
-  static constexpr int CAMAX = CAMAX_;
+  static constexpr int CAMAX = CAMAX_, LREF = LREF_;
 };
 using CfgRuntime = Cfg<-1, -1, -1, -1, -1, -1>;
-using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
-using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1>;  // C2: cosine-weighted only
+using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
+using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1>;  // C2: cosine-weighted only
+// The LREF constants (the host checks spt_params against them before it picks an LREF kernel).
+constexpr int kRefLightId = 6, kRefRrDepth = 5;
+constexpr float kRefLx0 = 32.0f, kRefLz0 = 63.0f, kRefLy = 81.6f, kRefLarea = 1296.0f;
+constexpr uint32_t kRefLdxi = 36u, kRefLdzi = 36u;
+template <class CF> __device__ __forceinline__ int light_id_of(const SPT_CONST KParams* P) {
+  if constexpr (CF::LREF == 1) return kRefLightId; else return P->light_id;
+}
+template <class CF> __device__ __forceinline__ int rr_depth_of(const SPT_CONST KParams* P) {
+  if constexpr (CF::LREF == 1) return kRefRrDepth; else return P->rr_depth;
+}
 template <class TP>
 __device__ __forceinline__ auto rects_of(const SPT_CONST SceneGeo* G) {
   if constexpr (TP::CONSTGEO) return CornellRectPtr{0};
@@ -614,7 +627,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     if (ls >= kStPath) {  // kStPath or kStShadow
       // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
       SPT_REGION(4);
-      const SPT_CONST SceneGeo* G = cptr(P->geo);
+      const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
       int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
       float t, ia_hit;
       bool hit = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, o, d, t, id, ia_hit);
@@ -632,10 +645,11 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       if (ls == kStShadow) {
         SPT_REGION(6);
         const SPT_CONST KParams* D = cptr(Pg);
-        const bool lh = id == D->light_id;
+        const bool lh = id == light_id_of<CF>(D);
         if (lh) SPT_REGION(7);
         l_hit += lh ? 1u : 0u;
-        const float pdf = fabsf(div_mk(D->larea * d.y, t * t));        // :471
+        const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
+        const float pdf = fabsf(div_mk(larea * d.y, t * t));            // :471
         const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
         const float w = lh ? pdf * brdf : 1.0f;
         T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
@@ -710,7 +724,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         // ends here.
         const int max_depth = CF::MAXD0 == 1 ? 0 : P->max_depth;
         const bool capd = (max_depth > 0) & (depth >= max_depth);
-        const bool rr = (depth > P->rr_depth) | (p == 0.0f);
+        const bool rr = (depth > rr_depth_of<CF>(P)) | (p == 0.0f);
         const bool alive = (p > 0.0f) & ((!(p < 1.0f)) | (u16(rl.x, rl.y) < p));
         const bool term = capd | (rr & !alive);
         const float ip = keep(H.ip);  // == 1.0f / p, read unconditionally (no branch)
@@ -787,18 +801,22 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
             float xl, zl;
             const int lmode = CF::LMODE >= 0 ? CF::LMODE : D->light_mode;
             if (lmode == SPT_LIGHT_GLIBC_WRAP) {
-              xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * D->ldxi), 0x1p-31f, D->lx0);
-              zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * D->ldzi), 0x1p-31f, D->lz0);
+              const uint32_t ldxi = CF::LREF == 1 ? kRefLdxi : D->ldxi;
+              const uint32_t ldzi = CF::LREF == 1 ? kRefLdzi : D->ldzi;
+              const float lx0 = CF::LREF == 1 ? kRefLx0 : D->lx0, lz0 = CF::LREF == 1 ? kRefLz0 : D->lz0;
+              xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * ldxi), 0x1p-31f, lx0);
+              zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * ldzi), 0x1p-31f, lz0);
             } else {
               xl = fmaf(u01(r.x), D->ldx, D->lx0);
               zl = fmaf(u01(r.y), D->ldz, D->lz0);
             }
-            const f3 dl = normalize3(mk(xl - x.x, D->ly - x.y, zl - x.z));
+            const float ly = CF::LREF == 1 ? kRefLy : D->ly;
+            const f3 dl = normalize3(mk(xl - x.x, ly - x.y, zl - x.z));
             l_nee += term ? 0u : 1u;
-            const SPT_CONST SceneGeo* G2 = cptr(D->geo);
+            const SPT_CONST SceneGeo* G2 = TP::CONSTGEO ? nullptr : cptr(D->geo);
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
             const bool la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
-            const bool cand = (id == D->light_id) | la;
+            const bool cand = (id == light_id_of<CF>(D)) | la;
             d = dl;  // a rejected lane generates its cosine direction next iteration anyway
             nxt = cand ? kStShadow : kStCos;
           }
@@ -1271,8 +1289,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   bool cam_axis = K.cam[7] == 0.0f && K.cam[8] == 0.0f && K.cam[9] == 0.0f && K.cam[11] == 0.0f &&
                   K.cam[0] != 0.0f && K.cam[1] != 0.0f && K.cam[2] != 0.0f;
   for (int i = 0; i < 12; ++i) cam_axis = cam_axis && std::isfinite(K.cam[i]);
+  const bool lref = p->rr_depth == kRefRrDepth && p->light_id == kRefLightId &&
+                    p->light_x0 == kRefLx0 && p->light_dx == 36.0f && p->light_z0 == kRefLz0 &&
+                    p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
   const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
-                        p->rr_depth >= 1 && cam_axis;
+                        p->rr_depth >= 1 && cam_axis && lref;
   int kv = KV_GENERIC;
   if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
   else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;

@@ -55,6 +55,8 @@ def test_small_image_bit_exact_and_stats(spt, oracle, est, q, fl):
     dict(width=40, height=30, spp=6, seed=7, rr_depth=0),           # RR from the first vertex
     dict(width=1, height=1, spp=64, seed=8),                        # single pixel
     dict(width=40, height=30, spp=6, seed=10, nee_prob=0.0, flags=1),  # uniform hemisphere only
+    dict(width=40, height=30, spp=6, seed=16, light_x0=40.0),       # non-reference light sample rect
+    dict(width=40, height=30, spp=6, seed=18, rr_depth=4),          # non-reference RR depth
 ])
 def test_edge_cases_bit_exact(spt, oracle, case):
     p = spt.default_params(**case)
