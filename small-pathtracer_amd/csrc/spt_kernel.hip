@@ -486,6 +486,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   f3 d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
   u4 r = u4{0, 0, 0, 0};  // Philox words of the vertex the pending path ray leads to
   // ---- wave-uniform state
+  // Camera and fixed-point constants of the axis-aligned camera kernels, loaded once and held in
+  // SGPRs (each scalar reload in the loop is a wait for the wave).
+  struct CamK { float o0, o1, o2, l0, l1, l2, h0, v1, iw, ih, fs; };
+  CamK ck{};
+  if constexpr (CF::CAMAX == 1) {
+    const SPT_CONST KParams* C = cptr(Pg);
+    ck = CamK{C->cam[0], C->cam[1], C->cam[2], C->cam[3], C->cam[4], C->cam[5], C->cam[6],
+              C->cam[10], C->inv_w, C->inv_h, C->fix_scale};
+  }
   uint32_t pool_next = 0, pool_end = 0;
   bool exhausted = false, capped = false;
   // Wave-uniform event counters (SGPRs), fed by ballots at convergent points of the loop: per-lane
@@ -528,7 +537,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
     // 1) retire finished units: flush the fixed-point sums of their pixel.
     if (ls == kStCam && s >= s_end) {
       SPT_REGION(1);
-      unsigned long long* a = P->accum + 3ull * lp;
+      unsigned long long* a = cptr(Pg)->accum + 3ull * lp;
       if (acc0) atomicAdd(a + 0, acc0);
       if (acc1) atomicAdd(a + 1, acc1);
       if (acc2) atomicAdd(a + 2, acc2);
@@ -598,13 +607,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       }
       {
         const SPT_CONST KParams* C = cptr(Pg);
-        const float su = (fx + u16(r.x, r.y)) * C->inv_w;
-        const float sv = (fy + u16(r.z, r.w)) * C->inv_h;
         f3 vc;
         if constexpr (CF::CAMAX == 1) {  // fma(+-0, s, a) == a for a != 0; a == +-0 only meets - o
-          vc = mk(fmaf(C->cam[6], su, C->cam[3]) - C->cam[0], fmaf(C->cam[10], sv, C->cam[4]) - C->cam[1],
-                  C->cam[5] - C->cam[2]);
+          const float su = (fx + u16(r.x, r.y)) * ck.iw;
+          const float sv = (fy + u16(r.z, r.w)) * ck.ih;
+          vc = mk(fmaf(ck.h0, su, ck.l0) - ck.o0, fmaf(ck.v1, sv, ck.l1) - ck.o1, ck.l2 - ck.o2);
         } else {
+          const float su = (fx + u16(r.x, r.y)) * C->inv_w;
+          const float sv = (fy + u16(r.z, r.w)) * C->inv_h;
           vc = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
                   fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
                   fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
@@ -836,7 +846,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           ls = kStSpec;
         } else {
           SPT_REGION(9);
-          const float scale = cptr(Pg)->fix_scale;
+          const float scale = CF::CAMAX == 1 ? ck.fs : cptr(Pg)->fix_scale;
           acc0 += fix31(L.x, scale);
           acc1 += fix31(L.y, scale);
           acc2 += fix31(L.z, scale);
@@ -846,7 +856,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           depth = 0;
           {
             const SPT_CONST KParams* C = cptr(Pg);
-            o = mk(C->cam[0], C->cam[1], C->cam[2]);  // the next sample's camera ray
+            o = CF::CAMAX == 1 ? mk(ck.o0, ck.o1, ck.o2) : mk(C->cam[0], C->cam[1], C->cam[2]);
           }
           if (TP::MAT) branch = 0;
           ls = kStCam;
