@@ -47,4 +47,5 @@ build smallpt_uni -e '340,347d' -e '351d' -e '360d'
 xs='530s/Xi\[3\] = { 0, 0, y \* y \* y }/Xi[3] = { 0, (unsigned short)seed_, (unsigned short)(y * y * y) }/'
 build smallpt_nee_xs -e "$xs"
 build smallpt_cos_xs -e '464s/if (q < 1)/if (q < 0)/' -e "$xs"
-echo "built $OUT/smallpt_{nee,cos,uni} $OUT/smallpt_{nee,cos}_xs"
+build smallpt_uni_xs -e '340,347d' -e '351d' -e '360d' -e "$xs"
+echo "built $OUT/smallpt_{nee,cos,uni} $OUT/smallpt_{nee,cos,uni}_xs"

@@ -26,7 +26,14 @@ BLOCK_Z2_MAX = 1.6
 def load_fixture():
     f = np.load(FIXTURE)  # plain arrays, allow_pickle=False
     w, h, spp, k = (int(v) for v in f["shape"])
-    return {"w": w, "h": h, "spp": spp, "k": k, "nee": f["nee_blocks"], "cos": f["cos_blocks"]}
+    return {"w": w, "h": h, "spp": spp, "k": k, "nee": f["nee_blocks"], "cos": f["cos_blocks"],
+            "uni": f["uni_blocks"]}  # uni: the uniform-hemisphere build (smallpt_uni_xs), NEE on
+
+
+def params_of(est):
+    """spt_params keyword arguments of an estimator name (nee / cos / uni)."""
+    return {"nee": dict(nee_prob=1.0), "cos": dict(nee_prob=0.0),
+            "uni": dict(nee_prob=1.0, flags=1)}[est]
 
 
 def blocks(img, k):

@@ -12,7 +12,8 @@ runs it, and stores (`--counter-only`: only the counter-mode pins, after a contr
                                oracle/_ref/smallpt_{nee,cos}_xs (row streams seeded too, so the runs
                                are independent) at 256x192@256, seeds 101..116, as 16x16-block means
                                of the linearised PPM ((v/255)^2.2): per-seed block means
-                               {est}_blocks (16, 12, 16, 3)
+                               {est}_blocks (16, 12, 16, 3); uni_blocks (the uniform-hemisphere
+                               build smallpt_uni_xs) added by `--fidelity-add uni`
 """
 import hashlib
 import json
@@ -58,6 +59,27 @@ def fidelity_fixture(ref, tmp, w=256, h=192, spp=256, seeds=range(101, 117), k=1
              seeds=np.array(list(seeds)), shape=np.array([w, h, spp, k]))
 
 
+def fidelity_add(ref, tmp, est, w=256, h=192, spp=256, seeds=range(101, 117), k=16):
+    """Add {est}_blocks (16 independent runs of oracle/_ref/smallpt_{est}_xs) to the existing P2
+    fixture, leaving its other arrays as they are (`--fidelity-add uni`)."""
+    from concurrent.futures import ThreadPoolExecutor
+    path = os.path.join(HERE, f"ref_fidelity_{w}x{h}_s{spp}.npz")
+    old = dict(np.load(path))  # plain arrays, allow_pickle=False
+    assert [int(v) for v in old["shape"]] == [w, h, spp, k]
+    assert list(old["seeds"]) == list(seeds)
+
+    def run(s):
+        p = os.path.join(tmp, f"fid_{est}_{s}.ppm")
+        subprocess.run([os.path.join(ref, f"smallpt_{est}_xs"), str(w), str(h), str(spp), str(s), p],
+                       check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        lin = (read_ppm(p) / 255.0) ** 2.2
+        return lin.reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+
+    with ThreadPoolExecutor(max(1, (os.cpu_count() or 2) - 1)) as ex:
+        old[f"{est}_blocks"] = np.array(list(ex.map(run, seeds)))
+    np.savez(path, **old)
+
+
 def counter_pins(out):
     """Counter-mode contract pins (oracle output) for the GPU regression tests."""
     from oracle import oracle as o
@@ -75,6 +97,13 @@ def counter_pins(out):
 
 
 def main():
+    if "--fidelity-add" in sys.argv:  # one more estimator in the P2 fixture (e.g. uni)
+        est = sys.argv[sys.argv.index("--fidelity-add") + 1]
+        subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
+        tmp = "/tmp/spt_golden"
+        os.makedirs(tmp, exist_ok=True)
+        fidelity_add(os.path.join(ROOT, "oracle", "_ref"), tmp, est)
+        return
     if "--counter-only" in sys.argv:  # contract change: re-pin the oracle's images, keep the rest
         path = os.path.join(HERE, "golden.json")
         out = json.load(open(path))

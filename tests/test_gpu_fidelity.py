@@ -13,15 +13,17 @@ import fidelity
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kernel", ["head", "const", "cornell", "generic"])
-@pytest.mark.parametrize("est", ["nee", "cos"])
+@pytest.mark.parametrize("kernel,est", [(k, e) for k in ("head", "const", "cornell", "generic")
+                                        for e in ("nee", "cos")] + [("generic", "uni")])
 def test_product_estimates_the_reference_image(spt, monkeypatch, est, kernel):
+    """uni: the uniform-hemisphere scattering (SPT_FLAG_UNIFORM_SCATTER, generic kernel) against the
+    reference built with its commented-out uniform body (smallpt_uni_xs)."""
     monkeypatch.setenv("SPT_KERNEL", kernel)
     fx = fidelity.load_fixture()
     w, h, spp, k = fx["w"], fx["h"], fx["spp"], fx["k"]
     own = []
     for seed in range(1, 17):
-        p = spt.default_params(width=w, height=h, spp=spp, seed=seed, nee_prob=1.0 if est == "nee" else 0.0)
+        p = spt.default_params(width=w, height=h, spp=spp, seed=seed, **fidelity.params_of(est))
         img = spt.render(spt.cornell_scene(), spt.Camera(aspect=w / h), p)
         own.append(fidelity.blocks(img, k))
     zg, z2 = fidelity.compare(fx[est], own)

@@ -228,7 +228,7 @@ def test_contract_path_statistics_match_reference(oracle, nee):
     assert 0.1 < ref["misses"] / n < 1.0
 
 
-@pytest.mark.parametrize("est", ["nee", "cos"])
+@pytest.mark.parametrize("est", ["nee", "cos", "uni"])
 def test_contract_fidelity_vs_reference_runs(oracle, est):
     """P2 for the contract itself (the CPU statement the GPU is bit-exact with): 4 seeds at
     256x192@256 against 16 independent runs of the reference binary (tests/fidelity.py)."""
@@ -237,7 +237,7 @@ def test_contract_fidelity_vs_reference_runs(oracle, est):
     w, h, spp, k = fx["w"], fx["h"], fx["spp"], fx["k"]
     own = []
     for seed in (1, 2, 3, 4):
-        p = oracle.default_params(width=w, height=h, spp=spp, seed=seed, nee_prob=1.0 if est == "nee" else 0.0)
+        p = oracle.default_params(width=w, height=h, spp=spp, seed=seed, **fidelity.params_of(est))
         img, _ = oracle.counter_render(oracle.scene_cornell(), oracle.camera(w / h), p)
         own.append(fidelity.blocks(img, k))
     zg, z2 = fidelity.compare(fx[est], own)
