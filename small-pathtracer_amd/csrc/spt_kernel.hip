@@ -534,16 +534,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       exhausted = true;
       ls = kStIdle;
     }
-    // 1) retire finished units: flush the fixed-point sums of their pixel.
-    if (ls == kStCam && s >= s_end) {
-      SPT_REGION(1);
-      unsigned long long* a = cptr(Pg)->accum + 3ull * lp;
-      if (acc0) atomicAdd(a + 0, acc0);
-      if (acc1) atomicAdd(a + 1, acc1);
-      if (acc2) atomicAdd(a + 2, acc2);
-      acc0 = acc1 = acc2 = 0;
-      ls = kStIdle;
-    }
+    // 1) (a unit is retired at the end of its last sample, in the path-end block below)
     // 2) refill idle lanes from the wave's pool (ballot + mbcnt prefix sum), pool from the queue.
     bool needs_unit = ls == kStIdle;
     uint64_t need = __ballot(needs_unit);
@@ -860,6 +851,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           }
           if (TP::MAT) branch = 0;
           ls = kStCam;
+          if (s >= s_end) {  // the unit's last sample: flush its pixel's fixed-point sums
+            SPT_REGION(1);
+            unsigned long long* a = cptr(Pg)->accum + 3ull * lp;
+            if (acc0) atomicAdd(a + 0, acc0);
+            if (acc1) atomicAdd(a + 1, acc1);
+            if (acc2) atomicAdd(a + 2, acc2);
+            acc0 = acc1 = acc2 = 0;
+            ls = kStIdle;
+          }
         }
       }
     }
