@@ -50,6 +50,15 @@ __global__ void __launch_bounds__(256) k_rate(uint32_t* out, uint32_t seed) {
     if constexpr (K == 17) { DO3("v_xad_u32") }
     if constexpr (K == 18) { DO3("v_perm_b32") }
     if constexpr (K == 19) { DO3("v_lshl_add_u32") }
+    if constexpr (K == 20) { DO1("v_cvt_f32_ubyte0") }
+    if constexpr (K == 21) { DO1("v_cvt_f32_ubyte1") }
+    if constexpr (K == 22) { DO3("v_bfi_b32") }
+    if constexpr (K == 23) { DO3("v_and_or_b32") }
+    if constexpr (K == 24) { DO3("v_lshl_or_b32") }
+    if constexpr (K == 25) { DO1("v_cvt_f32_i32") }
+    if constexpr (K == 26) { DO3("v_bfe_u32") }
+    if constexpr (K == 27) { DO("v_lshrrev_b32") }
+    if constexpr (K == 28) { DO("v_mul_u32_u24") }
   }
   out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
@@ -124,6 +133,8 @@ int main() {
   R32(7, "v_rcp_f32") R32(12, "v_rsq_f32") R32(8, "v_sin_f32") R32(9, "v_xor_b32")
   R32(10, "v_or3_b32") R32(13, "v_med3_f32") R32(14, "v_bitop3_b32") R32(15, "v_cvt_f32_u32")
   R32(16, "v_add3_u32") R32(17, "v_xad_u32") R32(18, "v_perm_b32") R32(19, "v_lshl_add_u32")
+  R32(20, "v_cvt_f32_ubyte0") R32(21, "v_cvt_f32_ubyte1") R32(22, "v_bfi_b32") R32(23, "v_and_or_b32")
+  R32(24, "v_lshl_or_b32") R32(25, "v_cvt_f32_i32") R32(26, "v_bfe_u32") R32(27, "v_lshrrev_b32")
   R64(0, "v_pk_fma_f32") R64(1, "v_pk_mul_f32") R64(2, "v_pk_add_f32") R64(3, "v_mad_u64_u32")
   R64(4, "v_fma_f64")
   printf("CUs %d clock %d kHz\n", ncu, p.clockRate);
