@@ -1241,6 +1241,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     const double want_units = 16.0 * lanes;
     const double per_pix = std::max(1.0, want_units / std::max(1, K.n_local_pix));
     chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
+    // ...but a unit should last >= ~200 lane-iterations: every unit costs a refill (~35 VALU +
+    // ~40 SALU for the whole wave) and a retire. Rays per sample at HEAD: 5.3 with NEE, 8.9
+    // cosine-only (C2: 6 -> 23 samples per unit, 4.73 -> ~4.6 ms; C3 stays at 48).
+    const double rays_per_sample = p->nee_prob > 0.0f ? 5.3 : 8.9;
+    chunk = std::max(chunk, (int)std::ceil(200.0 / rays_per_sample));
     chunk = std::min(chunk, p->spp);
   }
   K.chunk = chunk;
