@@ -77,36 +77,44 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
             "gpu_rows_bit_exact": bool(exact)}
 
 
-def reference_baseline(cfg, budget_s: float):
+def reference_baseline(cfg, budget_s: float, threads: int = 1):
     """The reference itself (oracle/_ref/smallpt_{nee,cos}: /root/reference/src/smallpt.cpp compiled
-    by oracle/build_ref.sh with the SURVEY Appendix A patch; single-threaded, as the reference's
-    OpenMP pragma :526 is commented out) on the same image size, with spp scaled to a bounded
-    sample of ~budget_s; None when the binary is absent (it is built only where the reference is)."""
+    by oracle/build_ref.sh with the SURVEY Appendix A patch) on the same image size, with spp scaled
+    to a bounded sample of ~budget_s; None when the binary is absent (it is built only where the
+    reference is). threads == 1: the build as shipped (its OpenMP pragma :526 is commented out).
+    threads > 1: the reference's own OpenMP loop (smallpt_*_omp: pragma :526 enabled, row loop
+    :528 made canonical) on that many host cores."""
     import subprocess
     import tempfile
 
     if cfg["scene"] != "cornell" or cfg["max_depth"] != 0:
         return None
-    binary = os.path.join(ROOT, "oracle", "_ref", "smallpt_nee" if cfg["nee_prob"] >= 1 else "smallpt_cos")
+    est = "nee" if cfg["nee_prob"] >= 1 else "cos"
+    binary = os.path.join(ROOT, "oracle", "_ref", f"smallpt_{est}" + ("_omp" if threads > 1 else ""))
     if not os.path.exists(binary):
         return None
     w, h = cfg["width"], cfg["height"]
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     with tempfile.TemporaryDirectory() as tmp:
         def run(spp):
             t0 = time.perf_counter()
             subprocess.run([binary, str(w), str(h), str(spp), "1", os.path.join(tmp, "o.ppm")],
-                           check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                           check=True, cwd=tmp, env=env, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
             return time.perf_counter() - t0
         spp = 1
         dt = run(spp)
         if dt < budget_s / 2:
             spp = max(2, int(budget_s / 2 / dt + 0.5))
             dt = run(spp)
-    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1,
+    how = ("single thread as shipped" if threads == 1 else
+           f"the reference's OpenMP loop (:526 enabled) on {threads} threads; its libc rand() is one "
+           f"locked global generator, so it scales negatively")
+    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
             "kind": "reference",
             "sample": f"{w}x{h} @ {spp} spp = {w * h * spp} samples in {dt:.1f} s (whole image incl. "
                       f"its P3 write); {os.path.relpath(binary, ROOT)} = the reference compiled from "
-                      f"its own sources, g++ -O3, single thread as shipped"}
+                      f"its own sources, g++ -O3, {how}"}
 
 
 def image_writer(spt, full, w, h, with_cpu: bool):
@@ -286,7 +294,10 @@ def main() -> None:
         port = None
         if not args.no_cpu_baseline and world == 1:
             cpu = reference_baseline(cfg, args.cpu_budget)
+            omp = reference_baseline(cfg, args.cpu_budget, threads=min(16, os.cpu_count() or 1))
             port = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
+            if cpu is not None and omp is not None:
+                cpu["openmp"] = omp
             if cpu is None:
                 cpu = port
             else:

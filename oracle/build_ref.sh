@@ -48,4 +48,16 @@ xs='530s/Xi\[3\] = { 0, 0, y \* y \* y }/Xi[3] = { 0, (unsigned short)seed_, (un
 build smallpt_nee_xs -e "$xs"
 build smallpt_cos_xs -e '464s/if (q < 1)/if (q < 0)/' -e "$xs"
 build smallpt_uni_xs -e '340,347d' -e '351d' -e '360d' -e "$xs"
-echo "built $OUT/smallpt_{nee,cos,uni} $OUT/smallpt_{nee,cos,uni}_xs"
+# the reference's own OpenMP loop (bench.py cpu_baseline): the pragma
+# :526 uncommented and the row loop :528 made canonical (i = y*w per row). rand() stays the
+# global, locked libc generator, as the reference would run it.
+omp=(-e '526s|// #pragma omp parallel for|#pragma omp parallel for|'
+     -e '528s/for (int y = 0, i = 0; y < h; y++) {/for (int y = 0; y < h; y++) { int i = y * w;/')
+buildomp() {
+  local bin=$1; shift
+  sed "${common_sed[@]}" "$@" "$REF/smallpt.cpp" \
+    | g++ -O3 -fopenmp -w -x c++ -I"$REF" - -o "$OUT/$bin"
+}
+buildomp smallpt_nee_omp "${omp[@]}"
+buildomp smallpt_cos_omp -e '464s/if (q < 1)/if (q < 0)/' "${omp[@]}"
+echo "built $OUT/smallpt_{nee,cos,uni} $OUT/smallpt_{nee,cos,uni}_xs $OUT/smallpt_{nee,cos}_omp"
