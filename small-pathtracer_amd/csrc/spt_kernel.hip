@@ -138,17 +138,20 @@ struct CornellRectPtr {
 // specialisations are all-DIFF, cosine-scatter scenes (keeps their cosine block branch-free).
 // NT*: rect tests per kind (parallel pairs count once).
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false,
-          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1>
+          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
   static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
-  static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = SPH_;
+  static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
 };
 // rect[] of :287-311 (light = XZ #3 -> pos 8); tests: 3 XY pairs, XZ floor/ceiling pair + light +
 // 2 box tops, 3 YZ pairs
 using TopoCornell = Topo<6, 5, 6, false, 8, false, 3, 4, 3>;
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
+// Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
+// no SPEC/REFR stack and branch words, 8 waves/SIMD instead of the generic kernel's 6.
+using TopoSphDiff = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, false>;
 
 // Estimator configuration the kernel is specialised for (compile-time where the host can prove
 // it, -1 = read from KParams at run time). Only wave-uniform branches and parameter loads go away;
@@ -938,11 +941,11 @@ static spt_status fail(spt_status s, const std::string& msg) {
 
 // Kernel variants, from the most general to the most specialised (SPT_KERNEL caps the level).
 using RenderFn = void (*)(const KParams*);
-enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_COUNT };
+enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
-    render_kernel<TopoCornellConst, CfgHeadCos>};
+    render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>};
 
 struct spt_context {
   int device = 0;
@@ -1314,6 +1317,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
   else if (cconst) kv = KV_CONST;
   else if (cornell) kv = KV_CORNELL;
+  else if (kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER)) kv = KV_SPHDIFF;
   const int grid = c->n_cu * c->bpc[kv];
   SPT_HIP(hipEventRecord(c->ev0, stream));
   hipLaunchKernelGGL(kRenderKernels[kv], dim3(grid), dim3(kBlock), 0, stream,

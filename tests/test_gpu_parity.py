@@ -65,8 +65,13 @@ def test_edge_cases_bit_exact(spt, oracle, case):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+@pytest.mark.parametrize("kernel", ["generic", "default"])
 @pytest.mark.parametrize("fl", [0, 1])
-def test_sphere_scene_bit_exact(spt, oracle, fl):
+def test_sphere_scene_bit_exact(spt, oracle, monkeypatch, fl, kernel):
+    """The 32-sphere scene: by default the all-DIFF sphere kernel (TopoSphDiff), the generic kernel
+    when capped or with the uniform-hemisphere flag; same contract, same bits."""
+    if kernel == "generic":
+        monkeypatch.setenv("SPT_KERNEL", "generic")
     p = spt.default_params(width=48, height=48, spp=8, seed=3, max_depth=16, flags=fl)
     gpu, gst, cpu, cst = _render_both(spt, oracle, spt.spheres32_scene(), p)
     _assert_exact(gpu, cpu)
