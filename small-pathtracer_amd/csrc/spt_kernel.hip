@@ -344,6 +344,11 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   (void)rect;
   if constexpr (TP::SPH) {
     const int nsph = G->n_sph, base = G->n_xy + G->n_xz + G->n_yz;
+#ifndef SPT_SPH_UNROLL
+#define SPT_SPH_UNROLL 8
+#endif
+    // unrolled so the scalar loads of several spheres are issued before one wait
+#pragma unroll SPT_SPH_UNROLL
     for (int j = 0; j < nsph; ++j) {
       const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
       const bool acc = kk < tmin_key;
