@@ -452,9 +452,12 @@ __device__ __forceinline__ T opq(T v) {
 // the NEE samples at HEAD); a lane whose shadow ray is pending simply skips the ray-generation and
 // shading blocks of that iteration. Per lane the arithmetic is exactly the counter-mode contract
 // (oracle c_path): only the schedule differs.
-//   iteration: [retire / refill units] -> [generate: cosine continuation or camera ray, one
-//   Philox call, shared normalize] -> [trace] -> [resolve a shadow ray] -> [shade a vertex: RR,
-//   NEE pre-test] -> [path end: accumulate].
+//   iteration: [refill idle lanes] -> [generate: cosine continuation and camera ray, one Philox
+//   call, shared normalize] -> [trace] -> [resolve a shadow ray] -> [shade a vertex: RR, NEE
+//   pre-test] -> [path end: accumulate; retire the unit after its last sample].
+// The lane state is one VGPR word (kSt*) and the small blocks are branch-free: the loop is bound
+// by instruction issue, and LLVM's exec-mask bookkeeping for loop-carried booleans and short
+// branches was SALU work on the CU's single scalar unit.
 template <class TP, class CF>
 __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
