@@ -131,6 +131,15 @@ spt_status spt_scene_spheres32(spt_prim* out, int32_t cap, int32_t* n_out);
 /* The room and light of :288-294 plus smallpt's mirror (SPEC) and glass (REFR) balls at the places
  * of the spheres commented out at :296-297; shading = the commented-out code :481-495. 9 prims. */
 spt_status spt_scene_cornell_specular(spt_prim* out, int32_t cap, int32_t* n_out);
+/* The classic smallpt sphere box of the reference's older revision (the constants mined from the
+ * shipped src/a.exe; its renders are the repository's image*.ppm): walls are
+ * spheres of radius 1e5 (left x = 1e5+1 green, right x = -1e5+99 red, back, front (black), floor,
+ * ceiling y = -1e5+81.6), a mirror and a glass ball of radius 16.5 at (27,16.5,47) / (73,16.5,78),
+ * and the light, a sphere of radius 600 at (50, 681.33, 81.6) with emission 12 (prim 8). 9 prims.
+ * Spheres of radius >= SPT_WIDE_SPHERE_RADIUS are intersected in fp64 (an fp32 quadratic cannot
+ * hold a 1e5 wall to the scene's scale). */
+spt_status spt_scene_smallpt_classic(spt_prim* out, int32_t cap, int32_t* n_out);
+#define SPT_WIDE_SPHERE_RADIUS 1000.0
 /* Rows rendered by this shard (params tile_rows/shard_index/shard_count), ascending. Returns count. */
 int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
 

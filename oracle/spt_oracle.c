@@ -535,6 +535,8 @@ typedef struct {
   float k;                 /* rect: plane coordinate */
   float ma, ha, mb, hb;    /* rect: in-plane bounds as |a - ma| <= ha, |b - mb| <= hb */
   float rad2, px, py, pz;  /* sphere */
+  double drad2, dpx, dpy, dpz; /* sphere in fp64 (wide: radius >= SPT_WIDE_SPHERE_RADIUS) */
+  int wide;
   fv e, c;
   float pmax;
   int refl;                /* spt_refl: DIFF, SPEC, REFR */
@@ -618,6 +620,22 @@ static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
  * nearer; the other one can only be the nearest hit of the two through the box's interior, i.e.
  * when the first plane's test is missed within an ulp of an edge. Every test then computes
  * t = n * inv_a exactly as a single rectangle (the same bits as testing that plane alone). */
+/* A wide sphere (the 1e5 walls of the classic smallpt box) in fp64: the cancellation-free
+ * quadratic with explicit fma, IEEE sqrt, the fp32 contract's epsilon, t rounded to float. */
+static float c_sphere_wide(const c_prim* P, fv o, fv d) {
+  const double ox = P->dpx - (double)o.x, oy = P->dpy - (double)o.y, oz = P->dpz - (double)o.z;
+  const double dx = d.x, dy = d.y, dz = d.z;
+  const double bb = fma(oz, dz, fma(oy, dy, ox * dx));
+  const double qx = fma(-bb, dx, ox), qy = fma(-bb, dy, oy), qz = fma(-bb, dz, oz);
+  const double det = P->drad2 - fma(qz, qz, fma(qy, qy, qx * qx));
+  double sd, t1, t2;
+  if (!(det >= 0.0)) return 0.0f;
+  sd = sqrt(det);
+  t1 = bb - sd;
+  t2 = bb + sd;
+  return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
+}
+
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   const float ix = spt_oracle_rcp_nr(d.x), iy = spt_oracle_rcp_nr(d.y), iz = spt_oracle_rcp_nr(d.z);
   float tmin = 1e20f;
@@ -654,9 +672,16 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
       }
     }
   }
-  for (i = 0; i < C->n; i++) {
-    const c_prim* P = &C->prims[i];
-    if (P->kind != SPT_SPHERE) continue;
+  /* Spheres in index order, the narrow (fp32) ones first, then the wide (fp64) ones. */
+  for (i = 0; i < 2 * C->n; i++) {
+    const int k = i % C->n;
+    const c_prim* P = &C->prims[k];
+    if (P->kind != SPT_SPHERE || P->wide != (i >= C->n)) continue;
+    if (P->wide) {
+      const float tt = c_sphere_wide(P, o, d);
+      if (tt != 0.0f && tt < tmin) { tmin = tt; *id = k; }
+      continue;
+    }
     { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
       const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
       const float bb = fdot(op, d);
@@ -668,7 +693,7 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
       t1 = bb - sd;
       t2 = bb + sd;
       tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
-      if (tt != 0.0f && tt < tmin) { tmin = tt; *id = i; }
+      if (tt != 0.0f && tt < tmin) { tmin = tt; *id = k; }
     }
   }
   *t = tmin;
@@ -968,6 +993,9 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
     if (s[i].kind == SPT_SPHERE) {
       P->rad2 = (float)s[i].geom[0] * (float)s[i].geom[0];
       P->px = (float)s[i].geom[1]; P->py = (float)s[i].geom[2]; P->pz = (float)s[i].geom[3];
+      P->wide = s[i].geom[0] >= SPT_WIDE_SPHERE_RADIUS;
+      P->drad2 = s[i].geom[0] * s[i].geom[0];
+      P->dpx = s[i].geom[1]; P->dpy = s[i].geom[2]; P->dpz = s[i].geom[3];
     } else {
       c_rect_mid(s[i].geom[0], s[i].geom[1], &P->ma, &P->ha);
       c_rect_mid(s[i].geom[2], s[i].geom[3], &P->mb, &P->hb);

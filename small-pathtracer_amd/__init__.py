@@ -89,7 +89,7 @@ STAT_KEYS = ["samples", "path_rays", "shadow_rays", "vertices", "nee_events", "n
 
 # Every entry point declared in include/spt.h (checked by tests/test_capi.py).
 EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_scene_spheres32",
-           "spt_scene_cornell_specular",
+           "spt_scene_cornell_specular", "spt_scene_smallpt_classic",
            "spt_shard_rows", "spt_render", "spt_context_create", "spt_context_destroy",
            "spt_context_reserve", "spt_render_async", "spt_context_stats", "spt_abi_version",
            "spt_status_string", "spt_last_error", "spt_device_count", "spt_image_bound",
@@ -123,6 +123,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.spt_scene_cornell.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_scene_spheres32.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_scene_cornell_specular.argtypes = [P(spt_prim), I32, P(I32)]
+    lib.spt_scene_smallpt_classic.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_shard_rows.argtypes = [P(spt_params), P(I32), I32]
     lib.spt_shard_rows.restype = I32
     lib.spt_render.argtypes = [P(spt_prim), I32, P(spt_camera), P(spt_params),
@@ -150,7 +151,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                  "spt_write_image"):
         getattr(lib, name).restype = I32
     for name in ("spt_default_params", "spt_camera_init", "spt_scene_cornell",
-                 "spt_scene_spheres32", "spt_scene_cornell_specular", "spt_render", "spt_context_create",
+                 "spt_scene_spheres32", "spt_scene_cornell_specular", "spt_scene_smallpt_classic",
+                 "spt_render", "spt_context_create",
                  "spt_context_destroy", "spt_context_reserve", "spt_render_async",
                  "spt_context_stats"):
         getattr(lib, name).restype = I32
@@ -257,6 +259,16 @@ def cornell_scene() -> list:
     arr = (spt_prim * 64)()
     n = ctypes.c_int32()
     _check(lib.spt_scene_cornell(arr, 64, ctypes.byref(n)))
+    return [arr[i] for i in range(n.value)]
+
+
+def smallpt_classic_scene() -> list:
+    """spt_scene_smallpt_classic(): the classic smallpt sphere box of the reference's older revision
+    (walls of radius 1e5, fp64-tested; mirror, glass and the radius-600 light sphere, prim 8)."""
+    lib = load_library()
+    arr = (spt_prim * 16)()
+    n = ctypes.c_int32()
+    _check(lib.spt_scene_smallpt_classic(arr, 16, ctypes.byref(n)))
     return [arr[i] for i in range(n.value)]
 
 

@@ -147,6 +147,33 @@ extern "C" spt_status spt_scene_cornell_specular(spt_prim* o, int32_t cap, int32
   return SPT_OK;
 }
 
+extern "C" spt_status spt_scene_smallpt_classic(spt_prim* o, int32_t cap, int32_t* n_out) {
+  if (!o || !n_out || cap < 9) return SPT_ERR_INVALID_ARG;
+  struct S { double r, x, y, z, e, c0, c1, c2; int refl; };
+  const S sc[9] = {
+      {1e5, 1e5 + 1, 40.8, 81.6, 0, .25, .75, .25, SPT_DIFF},   // left (green)
+      {1e5, -1e5 + 99, 40.8, 81.6, 0, .75, .25, .25, SPT_DIFF}, // right (red)
+      {1e5, 50, 40.8, 1e5, 0, .75, .75, .75, SPT_DIFF},         // back
+      {1e5, 50, 40.8, -1e5 + 170, 0, 0, 0, 0, SPT_DIFF},        // front
+      {1e5, 50, 1e5, 81.6, 0, .75, .75, .75, SPT_DIFF},         // floor
+      {1e5, 50, -1e5 + 81.6, 81.6, 0, .75, .75, .75, SPT_DIFF}, // ceiling
+      {16.5, 27, 16.5, 47, 0, .999, .999, .999, SPT_SPEC},      // mirror
+      {16.5, 73, 16.5, 78, 0, .999, .999, .999, SPT_REFR},      // glass
+      {600, 50, 681.6 - .27, 81.6, 12, 0, 0, 0, SPT_DIFF}};     // light
+  for (int k = 0; k < 9; ++k) {
+    spt_prim* p = &o[k];
+    std::memset(p, 0, sizeof *p);
+    p->kind = SPT_SPHERE;
+    p->refl = sc[k].refl;
+    p->geom[0] = sc[k].r;
+    p->geom[1] = sc[k].x; p->geom[2] = sc[k].y; p->geom[3] = sc[k].z;
+    p->e[0] = p->e[1] = p->e[2] = sc[k].e;
+    p->c[0] = sc[k].c0; p->c[1] = sc[k].c1; p->c[2] = sc[k].c2;
+  }
+  *n_out = 9;
+  return SPT_OK;
+}
+
 // Row-tile sharding: tile t (rows [t*T, t*T+T)) belongs to shard t % shard_count; a shard's rows
 // are listed in increasing order (the order of its compact output buffer).
 extern "C" int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap) {

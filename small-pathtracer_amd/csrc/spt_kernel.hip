@@ -66,15 +66,19 @@ static_assert(sizeof(DevPrim) == 64, "DevPrim layout");
 // rect bounds as |a - ma| <= ha, |b - mb| <= hb (c_rect_mid in the oracle): per axis one
 // subtract + one compare, each reading a single SGPR (the VALU constant-bus limit on gfx950).
 struct GeoRect { float k, ma, ha, mb, hb; int idx; int pad0, pad1; };   // 32 B
-struct GeoSph { float px, py, pz, rad2; int idx; int pad0, pad1, pad2; };  // 32 B
+struct GeoSph { float px, py, pz, rad2; int idx; int wide, pad1, pad2; };  // 32 B
+// fp64 geometry of a wide sphere (radius >= SPT_WIDE_SPHERE_RADIUS: the 1e5 walls of the classic
+// smallpt box), tested in double (oracle c_sphere_wide).
+struct GeoSphD { double px, py, pz, rad2; };
 // A rect test of the contract (oracle c_test): a parallel pair (k0 < k1, shared bounds) or a single
 // (k0 == k1, pos0 == pos1); pos* are grouped positions in rect[].
 struct GeoTest { float k0, k1, ma, ha, mb, hb; int pos0, pos1; };      // 32 B
 struct SceneGeo {
   int n_xy, n_xz, n_yz, n_sph;
-  int n_txy, n_txz, n_tyz, pad;  // rect tests per kind
+  int n_txy, n_txz, n_tyz, n_sph_wide;  // rect tests per kind; wide spheres = the last n_sph_wide
   GeoRect rect[kMaxPrims];  // [0,n_xy) XY, [n_xy, n_xy+n_xz) XZ, then YZ
   GeoSph sph[kMaxPrims];
+  GeoSphD sphd[kMaxPrims];
   GeoTest test[kMaxPrims];  // [0,n_txy) XY, then XZ, then YZ
 };
 #define SPT_CONST __attribute__((address_space(4)))
@@ -138,11 +142,12 @@ struct CornellRectPtr {
 // specialisations are all-DIFF, cosine-scatter scenes (keeps their cosine block branch-free).
 // NT*: rect tests per kind (parallel pairs count once).
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false,
-          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_>
+          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_, bool WIDE_ = false>
 struct Topo {
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
   static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
+  static constexpr bool WIDE = WIDE_;  // fp64 wide spheres may occur (their own kernel: VGPRs)
 };
 // rect[] of :287-311 (light = XZ #3 -> pos 8); tests: 3 XY pairs, XZ floor/ceiling pair + light +
 // 2 box tops, 3 YZ pairs
@@ -152,6 +157,9 @@ using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 // Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
 // no SPEC/REFR stack and branch words, 8 waves/SIMD instead of the generic kernel's 6.
 using TopoSphDiff = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, false>;
+// Scenes with wide spheres (radius >= SPT_WIDE_SPHERE_RADIUS, tested in fp64: the classic smallpt
+// box): the generic kernel plus the fp64 sphere loop, kept apart because the doubles cost VGPRs.
+using TopoGenericWide = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, true, true>;
 
 // Estimator configuration the kernel is specialised for (compile-time where the host can prove
 // it, -1 = read from KParams at run time). Only wave-uniform branches and parameter loads go away;
@@ -319,6 +327,25 @@ __device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d)
   return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
 }
 
+// A wide sphere (the 1e5 walls of the classic smallpt box) in fp64: the same cancellation-free
+// quadratic with explicit fma, an IEEE double sqrt, the fp32 contract's epsilon; t rounded to float
+// (oracle c_sphere_wide).
+__device__ __forceinline__ float sphere_t_wide(const SPT_CONST GeoSphD& S, f3 o, f3 d) {
+  const double ox = S.px - (double)o.x, oy = S.py - (double)o.y, oz = S.pz - (double)o.z;
+  const double dx = d.x, dy = d.y, dz = d.z;
+  const double bb = fma(oz, dz, fma(oy, dy, ox * dx));
+  const double qx = fma(-bb, dx, ox), qy = fma(-bb, dy, oy), qz = fma(-bb, dz, oz);
+  const double det = S.rad2 - fma(qz, qz, fma(qy, qy, qx * qx));
+  if (!(det >= 0.0)) return 0.0f;
+  const double sd = sqrt(det);
+  const double t1 = bb - sd, t2 = bb + sd;
+  return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
+}
+__device__ __forceinline__ float sphere_t_any(const SPT_CONST SceneGeo* G, int j, f3 o, f3 d) {
+  if (G->sph[j].wide) return sphere_t_wide(G->sphd[j], o, d);  // wave-uniform (scalar load)
+  return sphere_t(G->sph[j], o, d);
+}
+
 template <class TP>
 __device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; }
 
@@ -343,17 +370,25 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   }
   (void)rect;
   if constexpr (TP::SPH) {
-    const int nsph = G->n_sph, base = G->n_xy + G->n_xz + G->n_yz;
+    const int nsph = G->n_sph, nnar = nsph - G->n_sph_wide, base = G->n_xy + G->n_xz + G->n_yz;
 #ifndef SPT_SPH_UNROLL
 #define SPT_SPH_UNROLL 8
 #endif
     // unrolled so the scalar loads of several spheres are issued before one wait
 #pragma unroll SPT_SPH_UNROLL
-    for (int j = 0; j < nsph; ++j) {
+    for (int j = 0; j < nnar; ++j) {
       const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
       const bool acc = kk < tmin_key;
       tmin_key = acc ? kk : tmin_key;
       pos = acc ? base + j : pos;
+    }
+    if constexpr (TP::WIDE) {
+      for (int j = nnar; j < nsph; ++j) {  // wide spheres (fp64)
+        const uint32_t kk = tkey(sphere_t_wide(G->sphd[j], o, d));
+        const bool acc = kk < tmin_key;
+        tmin_key = acc ? kk : tmin_key;
+        pos = acc ? base + j : pos;
+      }
     }
   }
   const float tmin = __uint_as_float(tmin_key + 1u);
@@ -389,7 +424,8 @@ __device__ __forceinline__ bool light_accepts(const SPT_CONST KParams* P, const 
   } else {
     const int lk = P->light_kind, L = P->light_pos;
     if (L < 0) return false;
-    if (lk == SPT_SPHERE) return tkey(sphere_t(G->sph[L], o, d)) < tkey(1e20f);
+    if (lk == SPT_SPHERE)
+      return tkey(TP::WIDE ? sphere_t_any(G, L, o, d) : sphere_t(G->sph[L], o, d)) < tkey(1e20f);
     Ray6 r;
     if (lk == SPT_RECT_XY) r = Ray6{o.z, rcp_nr(d.z), d.x, o.x, d.y, o.y};
     else if (lk == SPT_RECT_XZ) r = Ray6{o.y, rcp_nr(d.y), d.x, o.x, d.z, o.z};
@@ -949,11 +985,12 @@ static spt_status fail(spt_status s, const std::string& msg) {
 
 // Kernel variants, from the most general to the most specialised (SPT_KERNEL caps the level).
 using RenderFn = void (*)(const KParams*);
-enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_COUNT };
+enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
-    render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>};
+    render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>,
+    render_kernel<TopoGenericWide, CfgRuntime>};
 
 struct spt_context {
   int device = 0;
@@ -1086,13 +1123,22 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
       }
     }
   }
+  // Spheres in index order, the narrow (fp32) ones first, then the wide (fp64) ones (oracle
+  // c_intersect): the kernel's fp32 loop carries no per-sphere precision test.
+  for (int pass = 0; pass < 2; ++pass)
   for (int i = 0; i < n; ++i) {
     if (s[i].kind != SPT_SPHERE) continue;
+    if ((s[i].geom[0] >= SPT_WIDE_SPHERE_RADIUS) != (pass == 1)) continue;
+    g->n_sph_wide += pass;
     GeoSph& S = g->sph[g->n_sph++];
     const float rad = (float)s[i].geom[0];
     S.px = (float)s[i].geom[1]; S.py = (float)s[i].geom[2]; S.pz = (float)s[i].geom[3];
     S.rad2 = rad * rad;
     S.idx = i;
+    S.wide = s[i].geom[0] >= SPT_WIDE_SPHERE_RADIUS ? 1 : 0;
+    GeoSphD& D = g->sphd[g->n_sph - 1];
+    D.px = s[i].geom[1]; D.py = s[i].geom[2]; D.pz = s[i].geom[3];
+    D.rad2 = s[i].geom[0] * s[i].geom[0];
     if (i == light) *light_pos = g->n_sph - 1;
   }
 }
@@ -1320,12 +1366,13 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                     p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
   const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
                         p->rr_depth >= 1 && cam_axis && lref;
-  int kv = KV_GENERIC;
+  int kv = g.n_sph_wide > 0 ? KV_WIDE : KV_GENERIC;  // (only the wide kernel has the fp64 loop)
   if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
   else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
   else if (cconst) kv = KV_CONST;
   else if (cornell) kv = KV_CORNELL;
-  else if (kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER)) kv = KV_SPHDIFF;
+  else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
+    kv = KV_SPHDIFF;
   const int grid = c->n_cu * c->bpc[kv];
   SPT_HIP(hipEventRecord(c->ev0, stream));
   hipLaunchKernelGGL(kRenderKernels[kv], dim3(grid), dim3(kBlock), 0, stream,

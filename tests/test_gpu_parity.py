@@ -65,6 +65,21 @@ def test_edge_cases_bit_exact(spt, oracle, case):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+@pytest.mark.parametrize("case", [
+    dict(width=48, height=36, spp=8, seed=21, nee_prob=0.0),              # pure path tracing
+    dict(width=40, height=30, spp=6, seed=22, nee_prob=1.0, light_id=8),  # :464 NEE to the sphere light
+    dict(width=32, height=24, spp=5, seed=23, nee_prob=0.0, max_depth=6, rr_depth=2),
+])
+def test_smallpt_classic_scene_bit_exact(spt, oracle, case):
+    """The classic smallpt sphere box (1e5-radius walls tested in fp64, mirror, glass, sphere
+    light) through the generic kernel against the oracle."""
+    p = spt.default_params(**case)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, spt.smallpt_classic_scene(), p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert gpu.mean() > 0.05 and gst["misses"] == 0  # a closed box: light reaches the image
+
+
 @pytest.mark.parametrize("kernel", ["generic", "default"])
 @pytest.mark.parametrize("fl", [0, 1])
 def test_sphere_scene_bit_exact(spt, oracle, monkeypatch, fl, kernel):
