@@ -106,6 +106,16 @@ inline std::vector<spt_prim> cornell_specular_scene() {
   return s;
 }
 
+// The classic smallpt sphere box of the reference's older revision (the shipped image*.ppm; the
+// constants of src/a.exe, spt_scene_smallpt_classic): 1e5-radius walls, light sphere = prim 8.
+inline std::vector<spt_prim> smallpt_classic_scene() {
+  std::vector<spt_prim> s(9);
+  int32_t n = 0;
+  spt_scene_smallpt_classic(s.data(), 9, &n);
+  s.resize(n);
+  return s;
+}
+
 inline double clamp(double x) { return x < 0 ? 0 : x > 1 ? 1 : x; }                 // :314-316
 inline int toInt(double x) { return int(std::pow(clamp(x), 1 / 2.2) * 255 + .5); }  // :319-321
 

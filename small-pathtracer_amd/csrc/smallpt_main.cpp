@@ -1,7 +1,9 @@
 // smallpt_main.cpp — the reference's main() (smallpt.cpp:502-557) on the MI355X:
-//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--uniform] [--specular] [--device N] [--p6 | --pfm]
+//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--uniform] [--specular | --classic] [--device N]
+//               [--p6 | --pfm]
 //   --uniform: random_scattering from the commented-out uniform hemisphere code (:352-359)
 //   --specular: smallpt's mirror and glass balls (SPEC/REFR, :481-495) in the HEAD room
+//   --classic: the classic smallpt sphere box of the shipped image*.ppm (pure path tracing)
 // Same scene, camera (:521), clamp/toInt and P3 output; the pixel loop is one spt_render() call.
 #include <chrono>
 #include <cstdlib>
@@ -15,12 +17,13 @@ using namespace smallpt_amd;
 int main(int argc, char* argv[]) {
   int pos[4] = {512, 512, 16, 1};  // :507-508 defaults, seed 1
   const char* out = "image.ppm";
-  bool cosine = false, uniform = false, specular = false;
+  bool cosine = false, uniform = false, specular = false, classic = false;
   int device = 0, npos = 0, format = SPT_IMAGE_P3;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--cos")) cosine = true;
     else if (!std::strcmp(argv[i], "--uniform")) uniform = true;
     else if (!std::strcmp(argv[i], "--specular")) specular = true;
+    else if (!std::strcmp(argv[i], "--classic")) classic = true;
     else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--p6")) format = SPT_IMAGE_P6;
     else if (!std::strcmp(argv[i], "--pfm")) format = SPT_IMAGE_PFM;
@@ -31,14 +34,15 @@ int main(int argc, char* argv[]) {
   spt_params p;
   spt_default_params(&p);
   p.width = pos[0]; p.height = pos[1]; p.spp = pos[2]; p.seed = (uint32_t)pos[3];
-  p.nee_prob = cosine ? 0.0f : 1.0f;  // :464
+  p.nee_prob = cosine || classic ? 0.0f : 1.0f;  // :464 (the classic box: emission only)
   if (uniform) p.flags |= SPT_FLAG_UNIFORM_SCATTER;
   p.device = device;
   Camera cam(LOOKFROM, Vec(50, 40, 5), Vec(0, 1, 0), 65, float(p.width) / float(p.height));  // :521
   spt_stats st{};
   std::vector<float> c;
   try {
-    c = render(specular ? cornell_specular_scene() : cornell_scene(), cam, p, &st);
+    c = render(classic ? smallpt_classic_scene() : specular ? cornell_specular_scene() : cornell_scene(),
+               cam, p, &st);
   } catch (const std::exception& e) {
     std::cerr << "render failed: " << e.what() << std::endl;
     return 1;
