@@ -14,6 +14,8 @@
 #   :548      output file name from argv[5]
 #   :464      (cosine variant only) q < 1  ->  q < 0
 #   :340-360  (uniform variant only) cosine body out, the commented uniform hemisphere body in
+#   :464      (Q = 0.5 variant) q < 1  ->  q < 0.5
+#   :19, :254, :295-310, :447  (sphere variants) see below
 # Pinned build: g++ -O3, x86-64 baseline (no -march=native: FMA contraction changes bits).
 set -euo pipefail
 REF=${REF:-/root/reference/src}
@@ -48,6 +50,10 @@ xs='530s/Xi\[3\] = { 0, 0, y \* y \* y }/Xi[3] = { 0, (unsigned short)seed_, (un
 build smallpt_nee_xs -e "$xs"
 build smallpt_cos_xs -e '464s/if (q < 1)/if (q < 0)/' -e "$xs"
 build smallpt_uni_xs -e '340,347d' -e '351d' -e '360d' -e "$xs"
+# NEE-mix probability Q = 0.5 (:464 `q < 1` -> `q < 0.5`: half light sampling, half cosine; the
+# estimator of the shipped image_32pps_halflighthalfimportance.ppm lineage)
+build smallpt_q05 -e '464s/if (q < 1)/if (q < 0.5)/'
+build smallpt_q05_xs -e '464s/if (q < 1)/if (q < 0.5)/' -e "$xs"
 # the reference's own OpenMP loop (bench.py cpu_baseline): the pragma
 # :526 uncommented and the row loop :528 made canonical (i = y*w per row). rand() stays the
 # global, locked libc generator, as the reference would run it.
@@ -60,4 +66,37 @@ buildomp() {
 }
 buildomp smallpt_nee_omp "${omp[@]}"
 buildomp smallpt_cos_omp -e '464s/if (q < 1)/if (q < 0)/' "${omp[@]}"
-echo "built $OUT/smallpt_{nee,cos,uni} $OUT/smallpt_{nee,cos,uni}_xs $OUT/smallpt_{nee,cos}_omp"
+
+# Config 5's 32-sphere scene rendered by the reference's OWN Sphere class (:223-254, fp64,
+# eps 1e-4) and its own radiance/intersect ("replace the rect[] initialiser
+# :287-311 with the 32-sphere scene using the reference's own Sphere class"):
+#   :19       NUMBER_OBJ 17 -> 39
+#   :295-310  the two boxes out; after the light (:294) the 32 spheres of spt_scene_spheres32
+#             (r = 6 at x = 1 + 98 (col + .5) / 8, y = 6, z = 30 + 30 row, colour pal[(3 row + col) % 8]),
+#             written with the same double expressions as small-pathtracer_amd/csrc/spt_host.cpp
+#   :254      Sphere gets the two Q-learning methods of the Hitable interface (:87-88), which it
+#             lacks (it would be abstract). They are never called: create_state_space is skipped
+#             (:517), and the methods return zeros.
+#   :447      (depth-capped variants) `if (depth + 1 >= D) return hit.e;` before the RR line :448:
+#             the path ends at vertex depth D with the hit's emission (spt_params.max_depth = D)
+sph_sed="$OUT/spheres32.sed"
+{
+  echo '19s/NUMBER_OBJ = 17;/NUMBER_OBJ = 39;/'
+  echo '254i\'
+  echo '	std::array<float, 3> add_key(Vec \&) const { return {0, 0, 0}; } std::array<float, 3> add_value(std::array<float, 3> \&) const { return {0, 0, 0}; }'
+  echo '295,310d'
+  echo '294a\'
+  pal=('.75, .25, .25' '.25, .75, .25' '.25, .25, .75' '.75, .75, .25' '.25, .75, .75' '.75, .25, .75' '.9, .9, .9' '.6, .45, .3')
+  for row in 0 1 2 3; do
+    for col in 0 1 2 3 4 5 6 7; do
+      sep=','; [ "$row$col" = 37 ] && sep=''
+      line="	new Sphere(6.0, Vec(1.0 + 98.0 * ($col + 0.5) / 8.0, 6.0, 30.0 + 30.0 * $row), Vec(), Vec(${pal[$(( (row * 3 + col) % 8 ))]}), DIFF)$sep"
+      [ "$row$col" = 37 ] && echo "$line" || echo "$line\\"
+    done
+  done
+} > "$sph_sed"
+build smallpt_sph -f "$sph_sed"
+build smallpt_sph_xs -f "$sph_sed" -e "$xs"
+build smallpt_sph16 -f "$sph_sed" -e '447a\	if (depth + 1 >= 16) return hit.e;'
+build smallpt_sph16_xs -f "$sph_sed" -e '447a\	if (depth + 1 >= 16) return hit.e;' -e "$xs"
+echo "built $OUT/smallpt_{nee,cos,uni,q05,sph,sph16} $OUT/smallpt_{nee,cos,uni,q05,sph,sph16}_xs $OUT/smallpt_{nee,cos}_omp"

@@ -81,19 +81,29 @@ def camera(aspect: float):
 
 
 def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, prims=None,
-                  uniform: bool = False, row_seed: bool = False, stats: bool = False):
+                  uniform: bool = False, row_seed: bool = False, stats: bool = False,
+                  qthr: float = None, max_depth: int = 0):
     """fp64 restatement of the reference (bit-exact with the patched oracle). (h, w, 3) float64.
 
     row_seed: seed erand48's row streams with the seed too (oracle/_ref/smallpt_cos_xs); without it
     the reference's scattering/RR draws are the same for every seed. stats: also return
-    {"vertices", "misses"} over all radiance() calls."""
+    {"vertices", "misses"} over all radiance() calls. qthr: the NEE-mix threshold of :464
+    (default 1 if nee else 0; oracle/_ref/smallpt_q05 is 0.5). max_depth: the depth cap of
+    oracle/_ref/smallpt_sph16 (0 = none, the reference)."""
     prims = prims or scene_cornell()
     arr = (_spt.spt_prim * len(prims))(*prims)
     out = np.zeros((h, w, 3), dtype=np.float64)
     st = (ctypes.c_uint64 * 2)()
-    flags = int(nee) | (2 if uniform else 0) | (4 if row_seed else 0)
-    lib().spt_oracle_compat_render_stats(arr, len(prims), w, h, spp, seed, flags,
-                                         out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), st)
+    flags = (2 if uniform else 0) | (4 if row_seed else 0)
+    if qthr is None:
+        qthr = 1.0 if nee else 0.0
+    L = lib()
+    L.spt_oracle_compat_render_ex.argtypes = [
+        ctypes.POINTER(_spt.spt_prim), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        ctypes.c_uint, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+    L.spt_oracle_compat_render_ex(arr, len(prims), w, h, spp, seed, flags, qthr, max_depth,
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), st)
     if stats:
         return out, {"vertices": int(st[0]), "misses": int(st[1])}
     return out
@@ -114,10 +124,29 @@ def counter_render(prims, cam, params, rows=None, threads: int = 0):
     rows = np.ascontiguousarray(rows, dtype=np.int32)
     arr = (_spt.spt_prim * len(prims))(*prims)
     out = np.zeros((len(rows), params.width, 3), dtype=np.float32)
-    st = (ctypes.c_uint64 * 8)()
+    st = (ctypes.c_uint64 * 10)()
     lib().spt_oracle_counter_render(arr, len(prims), ctypes.byref(cam), ctypes.byref(params),
                                     rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(rows),
                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), st, threads)
+    return out, dict(zip(_spt.STAT_KEYS, [int(v) for v in st]))
+
+
+def counter_render_pixels(prims, cam, params, pixels, threads: int = 0):
+    """Counter-mode contract at the listed pixels (y * w + x). Returns ((npix, 3) float32, stats)."""
+    pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
+    arr = (_spt.spt_prim * len(prims))(*prims)
+    out = np.zeros((len(pixels), 3), dtype=np.float32)
+    st = (ctypes.c_uint64 * 10)()
+    L = lib()
+    L.spt_oracle_counter_render_pixels.argtypes = [
+        ctypes.POINTER(_spt.spt_prim), ctypes.c_int, ctypes.POINTER(_spt.spt_camera),
+        ctypes.POINTER(_spt.spt_params), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    rc = L.spt_oracle_counter_render_pixels(
+        arr, len(prims), ctypes.byref(cam), ctypes.byref(params),
+        pixels.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(pixels),
+        out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), st, threads)
+    assert rc == 0
     return out, dict(zip(_spt.STAT_KEYS, [int(v) for v in st]))
 
 

@@ -129,7 +129,10 @@ typedef struct {
   const o_prim* prims;
   int n;
   int light_id;
-  int nee;     /* 1: `q < 1` (HEAD :464), 0: `q < 0` (cosine-only) */
+  double qthr; /* the NEE-mix threshold of :464: `q < 1` (HEAD), `q < 0` (cosine-only), or any
+                  other value (`q < 0.5`: oracle/build_ref.sh smallpt_q05) */
+  int max_depth; /* 0: none (HEAD); D > 0: `if (depth + 1 >= D) return hit.e;` before :448
+                    (oracle/build_ref.sh smallpt_sph16) */
   int uniform; /* random_scattering: 0 = cosine code :340-347, 1 = uniform code :352-359 */
   o_glibc_rand* g;
   uint64_t vertices, misses; /* radiance() calls and their misses (fidelity statistics) */
@@ -208,12 +211,13 @@ static dv o_radiance(const o_scene* S, dv ro, dv rd, int depth, unsigned short* 
     const double p = f.x > f.y && f.x > f.z ? f.x : f.y > f.z ? f.y : f.z;
     dv d;
     double q, PDF_inverse = 1, BRDF = 1;
+    if (S->max_depth > 0 && depth + 1 >= S->max_depth) return obj->e;
     if (++depth > 5 || !p) {
       if (o_erand48(Xi) < p) f = dmul(f, 1 / p);
       else return obj->e;
     }
     q = o_rand(S->g) / (double)O_RAND_MAX;
-    if (S->nee ? (q < 1) : (q < 0)) {
+    if (q < S->qthr) {
       d = o_light_sampling(S, x);
       d = dnorm(d);
       o_intersect(S, x, d, &t, &id);
@@ -268,14 +272,15 @@ void spt_oracle_camera(double out[12], const double lf[3], const double la[3], c
 }
 
 /* main() :502-542 with the HEAD scene, srand(seed) and the state-space build skipped.
- * nee: bit 0 = `q < 1` (HEAD) vs `q < 0`; bit 1 = uniform random_scattering (:352-359);
- * bit 2 = row streams {0, seed, y^3} instead of :530's {0, 0, y^3} (oracle/build_ref.sh
- * smallpt_cos_xs): without it every seed repeats the same scattering/RR draws and only rand()
- * varies, so seed-to-seed differences understate the estimator's noise.
- * c_out: w*h*3 doubles (clamped, row-major, y=0 top). stats (may be NULL): {vertices, misses}
- * over all radiance() calls. Returns 0. */
-int spt_oracle_compat_render_stats(const spt_prim* prims, int n, int w, int h, int spp,
-                                   unsigned seed, int nee, double* c_out, uint64_t* stats) {
+ * flags: bit 1 = uniform random_scattering (:352-359); bit 2 = row streams {0, seed, y^3}
+ * instead of :530's {0, 0, y^3} (oracle/build_ref.sh *_xs): without it every seed repeats the
+ * same scattering/RR draws and only rand() varies, so seed-to-seed differences understate the
+ * estimator's noise. qthr: the threshold of :464 (1 = HEAD NEE, 0 = cosine-only). max_depth: 0
+ * or the depth cap D of the capped builds. c_out: w*h*3 doubles (clamped, row-major, y=0 top).
+ * stats (may be NULL): {vertices, misses} over all radiance() calls. Returns 0. */
+int spt_oracle_compat_render_ex(const spt_prim* prims, int n, int w, int h, int spp, unsigned seed,
+                                int flags, double qthr, int max_depth, double* c_out,
+                                uint64_t* stats) {
   o_prim* P = (o_prim*)malloc(sizeof(o_prim) * (size_t)n);
   o_glibc_rand g;
   o_scene S;
@@ -284,7 +289,8 @@ int spt_oracle_compat_render_stats(const spt_prim* prims, int n, int w, int h, i
   int i, y;
   dv origin, llc, hor, ver;
   for (i = 0; i < n; i++) P[i] = o_from_spt(&prims[i]);
-  S.prims = P; S.n = n; S.light_id = 6; S.nee = nee & 1; S.uniform = (nee >> 1) & 1; S.g = &g;
+  S.prims = P; S.n = n; S.light_id = 6; S.qthr = qthr; S.max_depth = max_depth;
+  S.uniform = (flags >> 1) & 1; S.g = &g;
   S.vertices = S.misses = 0;
   o_srand(&g, seed);
   spt_oracle_camera(cam, lf, la, up, 65, (float)w / (float)h);
@@ -294,7 +300,7 @@ int spt_oracle_compat_render_stats(const spt_prim* prims, int n, int w, int h, i
   ver = dv3(cam[9], cam[10], cam[11]);
   for (y = 0, i = 0; y < h; y++) {
     unsigned short x, Xi[3];
-    Xi[0] = 0; Xi[1] = (nee & 4) ? (unsigned short)seed : 0; Xi[2] = (unsigned short)(y * y * y);
+    Xi[0] = 0; Xi[1] = (flags & 4) ? (unsigned short)seed : 0; Xi[2] = (unsigned short)(y * y * y);
     for (x = 0; x < w; x++) {
       dv r = dv3(0, 0, 0);
       int s;
@@ -314,6 +320,12 @@ int spt_oracle_compat_render_stats(const spt_prim* prims, int n, int w, int h, i
   if (stats) { stats[0] = S.vertices; stats[1] = S.misses; }
   free(P);
   return 0;
+}
+/* nee: bit 0 = `q < 1` (HEAD) vs `q < 0`; bits 1, 2 as the flags above. */
+int spt_oracle_compat_render_stats(const spt_prim* prims, int n, int w, int h, int spp,
+                                   unsigned seed, int nee, double* c_out, uint64_t* stats) {
+  return spt_oracle_compat_render_ex(prims, n, w, h, spp, seed, nee, (nee & 1) ? 1.0 : 0.0, 0,
+                                     c_out, stats);
 }
 int spt_oracle_compat_render(const spt_prim* prims, int n, int w, int h, int spp, unsigned seed,
                              int nee, double* c_out) {
@@ -636,6 +648,51 @@ static float c_sphere_wide(const c_prim* P, fv o, fv d) {
   return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
 }
 
+/* A narrow sphere in fp32: det = r^2 - |op - b d|^2 (cancellation-free form of :233), the nearest
+ * root beyond the fp32 epsilon 2e-3; 0 = no hit. */
+static float c_sphere(const c_prim* P, fv o, fv d) {
+  const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
+  const float bb = fdot(op, d);
+  const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
+  const float det = P->rad2 - fdot(q, q);
+  float sd, t1, t2;
+  if (!(det >= 0.0f)) return 0.0f;
+  sd = sqrtf(det);
+  t1 = bb - sd;
+  t2 = bb + sd;
+  return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+}
+
+/* Does the light itself accept the ray (o, d)? Its own test, exactly as inside c_intersect (the
+ * light is never paired). The device traces a NEE shadow ray only when this holds or the vertex
+ * lies on the light (id kept on a miss); otherwise the nearest hit cannot be the light (:467).
+ * Counts spt_stats.shadow_traced; never changes a result. */
+static int c_light_accepts(const c_ctx* C, fv o, fv d) {
+  const int l = C->P->light_id;
+  const c_prim* P;
+  if (l < 0 || l >= C->n) return 0;
+  P = &C->prims[l];
+  if (P->kind == SPT_SPHERE) {
+    const float tt = P->wide ? c_sphere_wide(P, o, d) : c_sphere(P, o, d);
+    return tt != 0.0f && tt < 1e20f;
+  }
+  {
+    float oa, da, tt, a, b;
+    switch (P->kind) {
+      case SPT_RECT_XY: oa = o.z; da = d.z; break;
+      case SPT_RECT_XZ: oa = o.y; da = d.y; break;
+      default: oa = o.x; da = d.x; break;
+    }
+    tt = (P->k - oa) * spt_oracle_rcp_nr(da);
+    switch (P->kind) {
+      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.y, tt, o.y - P->mb); break;
+      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
+      default: a = fmaf(d.y, tt, o.y - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
+    }
+    return fabsf(a) <= P->ha && fabsf(b) <= P->hb && (asu(tt) - 1u) < (asu(1e20f) - 1u);
+  }
+}
+
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   const float ix = spt_oracle_rcp_nr(d.x), iy = spt_oracle_rcp_nr(d.y), iz = spt_oracle_rcp_nr(d.z);
   float tmin = 1e20f;
@@ -682,17 +739,8 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
       if (tt != 0.0f && tt < tmin) { tmin = tt; *id = k; }
       continue;
     }
-    { /* sphere: det = r^2 - |op - b d|^2 (cancellation-free form of :233) */
-      const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
-      const float bb = fdot(op, d);
-      const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-      const float det = P->rad2 - fdot(q, q);
-      float sd, t1, t2, tt;
-      if (!(det >= 0.0f)) continue;
-      sd = sqrtf(det);
-      t1 = bb - sd;
-      t2 = bb + sd;
-      tt = t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+    {
+      const float tt = c_sphere(P, o, d);
       if (tt != 0.0f && tt < tmin) { tmin = tt; *id = k; }
     }
   }
@@ -758,7 +806,7 @@ static float c_div(float n, float d) {
 
 typedef struct {
   uint64_t samples, path_rays, shadow_rays, vertices, nee_events, nee_light_hits, cosine_samples,
-      misses;
+      misses, shadow_traced, sphere_vertices;
 } c_stats;
 
 /* A pending REFR branch (:494-495 at depth <= 2 returns reflection*Re + refraction*Tr): the
@@ -823,6 +871,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
       case SPT_RECT_XZ: nl = d.y < 0.0f ? fv3(0, 1, 0) : fv3(0, -1, 0); gn = fv3(0, 1, 0); break;
       case SPT_RECT_YZ: nl = d.x < 0.0f ? fv3(1, 0, 0) : fv3(-1, 0, 0); gn = fv3(1, 0, 0); break;
       default: {
+        st->sphere_vertices++;
         gn = fnormalize(fv3(x.x - H->px, x.y - H->py, x.z - H->pz));
         nl = fdot(gn, d) < 0.0f ? gn : fv3(-gn.x, -gn.y, -gn.z);
       }
@@ -927,6 +976,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
           zl = fmaf(u01(r[1]), P->light_dz, P->light_z0);
         }
         dl = fnormalize(fv3(xl - x.x, P->light_y - x.y, zl - x.z));
+        if (id == P->light_id || c_light_accepts(C, x, dl)) st->shadow_traced++;
         sh = c_intersect(C, x, dl, &ts, &ids);
         st->nee_events++;
         st->shadow_rays++;
@@ -1009,7 +1059,7 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
 }
 
 /* Render the rows listed in rows[0..nrows) (image row indices, y=0 top) of the counter-mode contract.
- * rgb_out: nrows*w*3 floats. stats_out: 8 uint64 in spt_stats order (may be NULL).
+ * rgb_out: nrows*w*3 floats. stats_out: 10 uint64 in spt_stats order (may be NULL).
  * threads <= 0: all OpenMP threads. Deterministic for any thread count. */
 int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* cam,
                               const spt_params* P, const int32_t* rows, int nrows, float* rgb_out,
@@ -1068,13 +1118,86 @@ int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* ca
       tot.samples += st.samples; tot.path_rays += st.path_rays; tot.shadow_rays += st.shadow_rays;
       tot.vertices += st.vertices; tot.nee_events += st.nee_events;
       tot.nee_light_hits += st.nee_light_hits; tot.cosine_samples += st.cosine_samples;
-      tot.misses += st.misses;
+      tot.misses += st.misses; tot.shadow_traced += st.shadow_traced;
+      tot.sphere_vertices += st.sphere_vertices;
     }
   }
   if (stats_out) {
     stats_out[0] = tot.samples; stats_out[1] = tot.path_rays; stats_out[2] = tot.shadow_rays;
     stats_out[3] = tot.vertices; stats_out[4] = tot.nee_events; stats_out[5] = tot.nee_light_hits;
     stats_out[6] = tot.cosine_samples; stats_out[7] = tot.misses;
+    stats_out[8] = tot.shadow_traced; stats_out[9] = tot.sphere_vertices;
+  }
+  free(CP);
+  return 0;
+}
+
+/* The counter-mode contract at a list of pixels (pixel = y * w + x, any order): rgb_out npix*3
+ * floats in list order, stats_out as spt_oracle_counter_render. Lets the GPU tests check a sample of
+ * pixels of a full-workload render (C4/C5: 1024-4096 spp) in seconds. */
+int spt_oracle_counter_render_pixels(const spt_prim* prims, int n, const spt_camera* cam,
+                                     const spt_params* P, const uint32_t* pixels, int npix,
+                                     float* rgb_out, uint64_t* stats_out, int threads) {
+  c_prim* CP;
+  c_ctx C;
+  c_test CT[64];
+  float camf[12];
+  const float inv_spp = 1.0f / (float)P->spp;
+  c_stats tot;
+  int i, pi;
+  if (n <= 0 || n > 64 || P->width <= 0) return -1;
+  CP = (c_prim*)malloc(sizeof(c_prim) * (size_t)n);
+  memset(&tot, 0, sizeof tot);
+  c_prims_from_spt(prims, n, CP);
+  C.prims = CP; C.n = n; C.P = P; C.key[0] = SPT_PHILOX_KEY0; C.key[1] = SPT_PHILOX_KEY1;
+  C.n_tests = c_build_tests(CP, n, P->light_id, CT);
+  C.tests = CT;
+  for (i = 0; i < 3; i++) {
+    camf[i] = (float)cam->origin[i];
+    camf[3 + i] = (float)cam->lower_left_corner[i];
+    camf[6 + i] = (float)cam->horizontal[i];
+    camf[9 + i] = (float)cam->vertical[i];
+  }
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#else
+  (void)threads;
+#endif
+#pragma omp parallel
+  {
+    c_stats st;
+    memset(&st, 0, sizeof st);
+#pragma omp for schedule(dynamic, 1)
+    for (pi = 0; pi < npix; pi++) {
+      const uint32_t pix = pixels[pi];
+      const int x = (int)(pix % (uint32_t)P->width), y = (int)(pix / (uint32_t)P->width);
+      uint64_t acc[3] = {0, 0, 0};
+      int s, ch;
+      for (s = 0; s < P->spp; s++) {
+        const fv L = c_path(&C, pix, (uint32_t)s, x, y, camf, &st);
+        acc[0] += c_fix(L.x, inv_spp);
+        acc[1] += c_fix(L.y, inv_spp);
+        acc[2] += c_fix(L.z, inv_spp);
+      }
+      for (ch = 0; ch < 3; ch++) {
+        const float v = (float)acc[ch] * 0x1p-31f;
+        rgb_out[(size_t)pi * 3 + (size_t)ch] = v > 1.0f ? 1.0f : v;
+      }
+    }
+#pragma omp critical
+    {
+      tot.samples += st.samples; tot.path_rays += st.path_rays; tot.shadow_rays += st.shadow_rays;
+      tot.vertices += st.vertices; tot.nee_events += st.nee_events;
+      tot.nee_light_hits += st.nee_light_hits; tot.cosine_samples += st.cosine_samples;
+      tot.misses += st.misses; tot.shadow_traced += st.shadow_traced;
+      tot.sphere_vertices += st.sphere_vertices;
+    }
+  }
+  if (stats_out) {
+    stats_out[0] = tot.samples; stats_out[1] = tot.path_rays; stats_out[2] = tot.shadow_rays;
+    stats_out[3] = tot.vertices; stats_out[4] = tot.nee_events; stats_out[5] = tot.nee_light_hits;
+    stats_out[6] = tot.cosine_samples; stats_out[7] = tot.misses;
+    stats_out[8] = tot.shadow_traced; stats_out[9] = tot.sphere_vertices;
   }
   free(CP);
   return 0;

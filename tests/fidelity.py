@@ -23,17 +23,38 @@ GLOBAL_Z_MAX = 4.0
 BLOCK_Z2_MAX = 1.6
 
 
+# Estimators pinned in the fixture: {name: (scene, spt_params keyword arguments, reference build)}.
+# Every reference build is oracle/_ref/smallpt_{name}_xs (oracle/build_ref.sh); the scene names
+# the product's builder (cornell_scene / spheres32_scene; the reference's own rect[] / the same
+# 32 spheres in the reference's own Sphere class).
+ESTIMATORS = {
+    "nee": ("cornell", dict(nee_prob=1.0)),                 # HEAD :464 q < 1
+    "cos": ("cornell", dict(nee_prob=0.0)),                 # :464 q < 0
+    "uni": ("cornell", dict(nee_prob=1.0, flags=1)),        # uniform hemisphere :352-359
+    "q05": ("cornell", dict(nee_prob=0.5)),                 # :464 q < 0.5 (NEE-mix Q)
+    "sph": ("spheres32", dict(nee_prob=1.0)),               # C5's scene, no depth cap
+    "sph16": ("spheres32", dict(nee_prob=1.0, max_depth=16)),  # C5: depth cap 16 (:447 + return)
+}
+
+
 def load_fixture():
     f = np.load(FIXTURE)  # plain arrays, allow_pickle=False
     w, h, spp, k = (int(v) for v in f["shape"])
-    return {"w": w, "h": h, "spp": spp, "k": k, "nee": f["nee_blocks"], "cos": f["cos_blocks"],
-            "uni": f["uni_blocks"]}  # uni: the uniform-hemisphere build (smallpt_uni_xs), NEE on
+    out = {"w": w, "h": h, "spp": spp, "k": k}
+    for est in ESTIMATORS:
+        if f"{est}_blocks" in f:
+            out[est] = f[f"{est}_blocks"]
+    return out
 
 
 def params_of(est):
-    """spt_params keyword arguments of an estimator name (nee / cos / uni)."""
-    return {"nee": dict(nee_prob=1.0), "cos": dict(nee_prob=0.0),
-            "uni": dict(nee_prob=1.0, flags=1)}[est]
+    """spt_params keyword arguments of an estimator name (ESTIMATORS)."""
+    return dict(ESTIMATORS[est][1])
+
+
+def scene_of(spt, est):
+    """The scene (prim list) of an estimator, from the product's builders."""
+    return spt.spheres32_scene() if ESTIMATORS[est][0] == "spheres32" else spt.cornell_scene()
 
 
 def blocks(img, k):

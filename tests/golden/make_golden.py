@@ -13,7 +13,9 @@ runs it, and stores (`--counter-only`: only the counter-mode pins, after a contr
                                are independent) at 256x192@256, seeds 101..116, as 16x16-block means
                                of the linearised PPM ((v/255)^2.2): per-seed block means
                                {est}_blocks (16, 12, 16, 3); uni_blocks (the uniform-hemisphere
-                               build smallpt_uni_xs) added by `--fidelity-add uni`
+                               build smallpt_uni_xs), q05_blocks (Q = 0.5), sph_blocks and
+                               sph16_blocks (config 5's 32-sphere scene in the reference's own
+                               Sphere class, uncapped / depth cap 16) added by `--fidelity-add <est>`
 """
 import hashlib
 import json
@@ -96,7 +98,83 @@ def counter_pins(out):
         out["counter_stats"][est] = st
 
 
+def variant_pins():
+    """md5s of the reference variants that need a scene or threshold argument in the restatement
+    (`--variant-pins`): smallpt_q05 (:464 q < 0.5), smallpt_sph (C5's 32 spheres in the reference's
+    own Sphere class), smallpt_sph16 (the same with the depth-16 cap), at 64x48@4 and 256x192@4,
+    seed 1, added to golden.json["reference_md5"] as {w}x{h}_s4_seed1_{variant}."""
+    subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
+    ref = os.path.join(ROOT, "oracle", "_ref")
+    tmp = "/tmp/spt_golden"
+    os.makedirs(tmp, exist_ok=True)
+    path = os.path.join(HERE, "golden.json")
+    out = json.load(open(path))
+    for w, h in ((64, 48), (256, 192)):
+        for est in ("q05", "sph", "sph16"):
+            ppm = os.path.join(tmp, f"ref_{w}x{h}_s4_{est}.ppm")
+            subprocess.run([os.path.join(ref, f"smallpt_{est}"), str(w), str(h), "4", "1", ppm],
+                           check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            out["reference_md5"][f"{w}x{h}_s4_seed1_{est}"] = md5(ppm)
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+
+
+def quality_c3(ref, tmp, w=1024, h=768, spp=64, seeds=range(201, 217), k=32):
+    """bench.py's `quality` fixture (`--quality-c3`): the reference's own C3 image (HEAD NEE,
+    1024x768) as 32x32-block means of its linearised PPM, one set per independent run of
+    oracle/_ref/smallpt_nee_xs at 64 spp (16 runs = 1024 spp pooled): ref_c3_blocks_k32.npz."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(s):
+        path = os.path.join(tmp, f"q_{s}.ppm")
+        subprocess.run([os.path.join(ref, "smallpt_nee_xs"), str(w), str(h), str(spp), str(s), path],
+                       check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        lin = (read_ppm(path) / 255.0) ** 2.2
+        os.remove(path)
+        return lin.reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+
+    with ThreadPoolExecutor(max(1, (os.cpu_count() or 2) - 1)) as ex:
+        blocks = np.array(list(ex.map(run, seeds)))
+    np.savez(os.path.join(HERE, f"ref_c3_blocks_k{k}.npz"), blocks=blocks, seeds=np.array(list(seeds)),
+             shape=np.array([w, h, spp, k]))
+
+
+SHIPPED = ["image_512pps_explicitlight", "image_512pps_explicitlight_test", "image_512pps_random_test",
+           "image2_32pps_importancesampl", "image2_32pps_explicitsampling", "image_32pps_totalrandom",
+           "image_32pps_halflighthalfimportance", "image1_16ssp_importsampl",
+           "image2_16ssp_explicitsampling"]
+
+
+def shipped_blocks(k=32):
+    """`--shipped`: the reference's shipped renders of the classic sphere box (/root/reference/*.ppm,
+    512x512 P3; renders of an older revision) as data: per image the
+    32x32-block means and within-block pixel variances of the linearised PPM ((v/255)^2.2):
+    shipped_sphere_box_k32.npz {name}_mean, {name}_var (16, 16, 3)."""
+    out = {}
+    for name in SHIPPED:
+        lin = (read_ppm(os.path.join("/root/reference", name + ".ppm")) / 255.0) ** 2.2
+        h, w, _ = lin.shape
+        b = lin.reshape(h // k, k, w // k, k, 3)
+        out[f"{name}_mean"] = b.mean(axis=(1, 3))
+        out[f"{name}_var"] = b.var(axis=(1, 3), ddof=1)
+    out["names"] = np.array(SHIPPED)
+    out["shape"] = np.array([512, 512, k])
+    np.savez(os.path.join(HERE, f"shipped_sphere_box_k{k}.npz"), **out)
+
+
 def main():
+    if "--shipped" in sys.argv:
+        shipped_blocks()
+        return
+    if "--quality-c3" in sys.argv:
+        subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
+        tmp = "/tmp/spt_golden"
+        os.makedirs(tmp, exist_ok=True)
+        quality_c3(os.path.join(ROOT, "oracle", "_ref"), tmp)
+        return
+    if "--variant-pins" in sys.argv:
+        variant_pins()
+        return
     if "--fidelity-add" in sys.argv:  # one more estimator in the P2 fixture (e.g. uni)
         est = sys.argv[sys.argv.index("--fidelity-add") + 1]
         subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)

@@ -57,6 +57,35 @@ def test_compat_restatement_matches_reference_binary_other_seeds(oracle, tmp_pat
         assert _md5_of_ppm(oracle, img, tmp_path, "c.ppm") == hashlib.md5(open(ref_path, "rb").read()).hexdigest()
 
 
+@pytest.mark.parametrize("w,h", [(64, 48), (256, 192)])
+@pytest.mark.parametrize("est", ["q05", "sph", "sph16"])
+def test_compat_restatement_matches_reference_variants_md5(oracle, spt, tmp_path, w, h, est):
+    """P0 for the reference variants built by oracle/build_ref.sh beyond HEAD: NEE-mix Q = 0.5
+    (:464 `q < 0.5`), config 5's 32 spheres in the reference's own Sphere class (:223-254, fp64,
+    eps 1e-4), and the same with the depth-16 cap."""
+    prims = spt.spheres32_scene() if est.startswith("sph") else None
+    img = oracle.compat_render(w, h, 4, seed=1, prims=prims, qthr=0.5 if est == "q05" else 1.0,
+                               max_depth=16 if est == "sph16" else 0)
+    assert _md5_of_ppm(oracle, img, tmp_path, "c.ppm") == GOLD["reference_md5"][f"{w}x{h}_s4_seed1_{est}"]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_DIR, "smallpt_sph")),
+                    reason="oracle/_ref not built (reference absent)")
+@pytest.mark.parametrize("est", ["q05", "sph", "sph16"])
+def test_compat_variants_match_reference_binary_other_seeds(oracle, spt, tmp_path, est):
+    """The same variants against the live reference binaries at an odd size and other seeds, plus
+    their row-seeded (_xs) builds (the P2 fixture's runs)."""
+    prims = spt.spheres32_scene() if est.startswith("sph") else None
+    kw = dict(prims=prims, qthr=0.5 if est == "q05" else 1.0, max_depth=16 if est == "sph16" else 0)
+    for seed, xs in ((7, False), (9, True)):
+        ref_path = str(tmp_path / "ref.ppm")
+        subprocess.run([os.path.join(REF_DIR, f"smallpt_{est}" + ("_xs" if xs else "")), "33", "17",
+                        "5", str(seed), ref_path], check=True, cwd=str(tmp_path),
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        img = oracle.compat_render(33, 17, 5, seed=seed, row_seed=xs, **kw)
+        assert _md5_of_ppm(oracle, img, tmp_path, "c.ppm") == hashlib.md5(open(ref_path, "rb").read()).hexdigest()
+
+
 def test_erand48_kat(oracle):
     for xi2, expect in GOLD["kat"]["erand48_row_seeds"].items():
         got = oracle.erand48_seq(int(xi2), 3)
@@ -228,17 +257,20 @@ def test_contract_path_statistics_match_reference(oracle, nee):
     assert 0.1 < ref["misses"] / n < 1.0
 
 
-@pytest.mark.parametrize("est", ["nee", "cos", "uni"])
-def test_contract_fidelity_vs_reference_runs(oracle, est):
+@pytest.mark.parametrize("est", ["nee", "cos", "uni", "q05", "sph16", "sph"])
+def test_contract_fidelity_vs_reference_runs(oracle, spt, est):
     """P2 for the contract itself (the CPU statement the GPU is bit-exact with): 4 seeds at
-    256x192@256 against 16 independent runs of the reference binary (tests/fidelity.py)."""
+    256x192@256 against 16 independent runs of the reference binary (tests/fidelity.py).
+    sph/sph16: the 32-sphere scene of config 5, whose fp32 sphere test (eps 2e-3) is pinned here
+    against the reference's own fp64 Sphere::intersect (eps 1e-4, :229-239)."""
     import fidelity
     fx = fidelity.load_fixture()
     w, h, spp, k = fx["w"], fx["h"], fx["spp"], fx["k"]
+    prims = fidelity.scene_of(spt, est)
     own = []
     for seed in (1, 2, 3, 4):
         p = oracle.default_params(width=w, height=h, spp=spp, seed=seed, **fidelity.params_of(est))
-        img, _ = oracle.counter_render(oracle.scene_cornell(), oracle.camera(w / h), p)
+        img, _ = oracle.counter_render(prims, oracle.camera(w / h), p)
         own.append(fidelity.blocks(img, k))
     zg, z2 = fidelity.compare(fx[est], own)
     assert np.all(np.abs(zg) < fidelity.GLOBAL_Z_MAX), zg
