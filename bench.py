@@ -49,12 +49,61 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_threads() -> int:
+    """CPU-baseline threads: the cores this process may run on, capped at 16 = one GPU's share of a
+    GPU-box host (the gpurun pool gives each GPU 16 cores; nproc reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+QUALITY_FIXTURE = os.path.join(ROOT, "tests", "golden", "ref_c3_blocks_k32.npz")
+
+
+def quality(img: np.ndarray, spp: int):
+    """The metric's quality half (BASELINE.json: per-channel RMSE vs the reference PPM) at C3:
+    the GPU image, quantised and linearised as the reference's P3 (toInt :319-321, (v/255)^2.2),
+    as 32x32-block means against the pooled block means of 16 independent runs of the reference
+    itself (oracle/_ref/smallpt_nee_xs, 1024x768 @ 64 spp each; tests/golden/ref_c3_blocks_k32.npz,
+    made by tests/golden/make_golden.py --quality-c3). Both images are Monte-Carlo estimates, so
+    the RMSE has a noise floor: the expected RMSE of two unbiased estimates at these sample counts,
+    from the spread of the 16 runs (per block: var_run * (64/spp + 1/16)); and the same RMSE
+    between the two halves of the reference runs (reference vs reference)."""
+    if not os.path.exists(QUALITY_FIXTURE):
+        return None
+    f = np.load(QUALITY_FIXTURE)  # plain arrays (allow_pickle=False)
+    blocks, (w, h, spp_ref, k) = f["blocks"], [int(v) for v in f["shape"]]
+    if img.shape != (h, w, 3):
+        return None
+    v = np.floor(np.power(np.clip(img.astype(np.float64), 0, 1), 1 / 2.2) * 255 + 0.5)
+    own = ((v / 255.0) ** 2.2).reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+    n = len(blocks)
+    ref = blocks.mean(0)
+    var_run = blocks.var(0, ddof=1)
+    rmse = np.sqrt(((own - ref) ** 2).mean(axis=(0, 1)))
+    floor = np.sqrt((var_run * (spp_ref / spp + 1.0 / n)).mean(axis=(0, 1)))
+    half = np.sqrt(((blocks[: n // 2].mean(0) - blocks[n // 2:].mean(0)) ** 2).mean(axis=(0, 1)))
+    half_floor = np.sqrt((var_run * (4.0 / n)).mean(axis=(0, 1)))
+    return {"rmse_vs_reference": [round(float(x), 6) for x in rmse],
+            "noise_floor": [round(float(x), 6) for x in floor],
+            "ratio_to_floor": [round(float(a / b), 3) for a, b in zip(rmse, floor)],
+            "reference_halves_rmse": [round(float(x), 6) for x in half],
+            "reference_halves_floor": [round(float(x), 6) for x in half_floor],
+            "mean_diff": [round(float(x), 6) for x in (own - ref).mean(axis=(0, 1))],
+            "rmse_vs_contract": None,
+            "space": f"linear, quantised as the reference's P3, {k}x{k}-block means, per channel (R,G,B)",
+            "reference": f"{n} runs of oracle/_ref/smallpt_nee_xs at {w}x{h} @ {spp_ref} spp "
+                         f"({n * spp_ref} spp pooled), tests/golden/{os.path.basename(QUALITY_FIXTURE)}"}
+
+
 def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
     """Counter-mode oracle (the same algorithm and random stream as the kernel) on the host cores,
     OpenMP over a cyclic row subset, sized to ~budget_s; also checks those rows bit-exactly."""
     from oracle import oracle
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     h, w, spp = params.height, params.width, params.spp
     # Grow an evenly spread row subset until one timed run takes >= budget_s / 2 (the first,
     # one-row-per-thread run also absorbs library load and OpenMP start-up).
@@ -70,7 +119,7 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
     samples = len(rows) * w * spp
     exact = gpu_img is not None and np.array_equal(gpu_img[rows], img)
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-            "kind": "port",
+            "host_cpus": os.cpu_count(), "kind": "port",
             "sample": f"{len(rows)} of {h} rows evenly spread, {w}x{spp} spp each = "
                       f"{samples} samples in {dt:.1f} s; oracle/spt_oracle.c counter mode, "
                       f"OpenMP dynamic rows",
@@ -111,7 +160,7 @@ def reference_baseline(cfg, budget_s: float, threads: int = 1):
            f"the reference's OpenMP loop (:526 enabled) on {threads} threads; its libc rand() is one "
            f"locked global generator, so it scales negatively")
     return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-            "kind": "reference",
+            "host_cpus": os.cpu_count(), "kind": "reference",
             "sample": f"{w}x{h} @ {spp} spp = {w * h * spp} samples in {dt:.1f} s (whole image incl. "
                       f"its P3 write); {os.path.relpath(binary, ROOT)} = the reference compiled from "
                       f"its own sources, g++ -O3, {how}"}
@@ -227,15 +276,23 @@ def main() -> None:
     stream = torch.cuda.current_stream()
     shard = torch.zeros((max_rows, w, 3), dtype=torch.float32, device="cuda")
     full = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
-    gather_list = ([torch.empty_like(shard) for _ in range(world)] if (rank == 0 and world > 1)
-                   else None)
+    comm = None
+    if world > 1 and backend == "nccl":
+        # the framebuffer gather of SURVEY §8e in the library (spt_comm: C++ over RCCL, grouped
+        # ncclSend/ncclRecv to rank 0 + the de-interleave kernel); torch.distributed only carries
+        # the RCCL unique id from rank 0 to the others
+        uid = [spt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = spt.Comm(uid[0], world, rank, local)
+        comm.reserve(params)
     kstats = []
 
     def step():
         ren.render_async(prims, cam, params, shard.data_ptr(), stream.cuda_stream)
         kstats.append(ren.stats())
-        if world > 1 and backend == "nccl":
-            sd.gather_rows(shard, rows_of, full, gather_list)  # one RCCL gather to rank 0
+        if comm is not None:  # one RCCL gather to rank 0, on the render's stream
+            comm.gather(params, shard.data_ptr(), full.data_ptr() if rank == 0 else 0,
+                        stream.cuda_stream)
         elif world > 1:
             host = sd.gather_rows(shard.cpu(), rows_of, full.cpu() if rank == 0 else None)
             if rank == 0:
@@ -266,7 +323,9 @@ def main() -> None:
     value = samples_per_step * args.steps / elapsed / 1e6
     kms = np.array([s["kernel_ms"] for s in kstats])
     flop = np.array([s["flop"] for s in kstats])
+    flop_x = np.array([s["flop_executed"] for s in kstats])
     achieved = float((flop / (kms * 1e-3)).mean() / 1e12)
+    achieved_x = float((flop_x / (kms * 1e-3)).mean() / 1e12)
     s0 = kstats[-1]
     my_samples = len(my_rows) * w * spp
     assert s0["samples"] == my_samples, (s0["samples"], my_samples)
@@ -294,7 +353,7 @@ def main() -> None:
         port = None
         if not args.no_cpu_baseline and world == 1:
             cpu = reference_baseline(cfg, args.cpu_budget)
-            omp = reference_baseline(cfg, args.cpu_budget, threads=min(16, os.cpu_count() or 1))
+            omp = reference_baseline(cfg, args.cpu_budget, threads=host_threads())
             port = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
             if cpu is not None and omp is not None:
                 cpu["openmp"] = omp
@@ -305,6 +364,10 @@ def main() -> None:
         if args.save_ppm:
             spt.write_ppm(args.save_ppm, img)
         writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)
+        qual = quality(img, spp) if (args.config == "c3" and world == 1) else None
+        if qual is not None and port is not None:
+            # the bench's own rows re-rendered by the CPU contract (cpu_baseline.port): exact
+            qual["rmse_vs_contract"] = 0.0 if port.get("gpu_rows_bit_exact") else None
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -321,6 +384,10 @@ def main() -> None:
                                       if world > 1 else "1 GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         # the same model with only the shadow rays the kernel traces charged a
+                         # scene test (the rest are rejected exactly by the light pre-test)
+                         "achieved_executed": round(achieved_x, 3),
+                         "frac_executed": round(achieved_x / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic,
                          "hbm_gbs": (round(traffic / (kms.mean() * 1e-3) / 1e9, 2)
                                      if traffic else None),
@@ -337,12 +404,17 @@ def main() -> None:
                          "flop_per_sample": round(float(flop.mean()) / my_samples, 1)},
             "paths": {"vertices_per_sample": round(s0["vertices"] / my_samples, 4),
                       "rays_per_sample": round((s0["path_rays"] + s0["shadow_rays"]) / my_samples, 4),
+                      "rays_traced_per_sample": round((s0["path_rays"] + s0["shadow_traced"])
+                                                      / my_samples, 4),
                       "misses_per_sample": round(s0["misses"] / my_samples, 4)},
+            "quality": qual,
             "cpu_baseline": cpu,
             "image_writer": writer,
         }
         print(json.dumps(out), flush=True)
     ren.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

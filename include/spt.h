@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 1
+#define SPT_ABI_VERSION 2 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed */
 
 typedef enum spt_status {
   SPT_OK = 0,
@@ -33,7 +33,8 @@ typedef enum spt_status {
   SPT_ERR_HIP = 2,         /* a HIP runtime call failed (spt_last_error() has the text) */
   SPT_ERR_NO_DEVICE = 3,   /* no usable gfx950 device */
   SPT_ERR_OOM = 4,         /* device allocation failed */
-  SPT_ERR_UNSUPPORTED = 5  /* reserved: feature not implemented (not returned today) */
+  SPT_ERR_UNSUPPORTED = 5, /* reserved: feature not implemented (not returned today) */
+  SPT_ERR_RCCL = 6         /* an RCCL call of the multi-GPU gather failed (spt_last_error()) */
 } spt_status;
 
 /* Primitive kinds: the reference's Hitable subclasses (:92-254). */
@@ -100,6 +101,13 @@ typedef struct spt_params {
  * dir = u cos(r1) sqrt(r2(2-r2)) + v sin(r1) sqrt(r2(2-r2)) + w (1-r2)) instead of the live
  * cosine-weighted code (:340-347); the estimator weight stays 1, as in the reference. */
 #define SPT_FLAG_UNIFORM_SCATTER 1u
+/* Kernel specialisation cap, flags bits 8-9 (A/B comparisons and tests; never changes a result:
+ * every kernel computes the same contract bit for bit). AUTO (0) runs the most specialised kernel
+ * the host can prove applicable to the scene and params; the others stop at that level. */
+#define SPT_FLAG_KERNEL_LEVEL_MASK 0x300u
+#define SPT_FLAG_KERNEL_LEVEL(l) (((uint32_t)(l) & 3u) << 8)
+enum { SPT_KERNEL_LEVEL_AUTO = 0, SPT_KERNEL_LEVEL_GENERIC = 1, SPT_KERNEL_LEVEL_CORNELL = 2,
+       SPT_KERNEL_LEVEL_CONST = 3 };
 
 /* Philox4x32-10 key (fixed, so the key schedule is compile-time) and counter layout:
  * ctr = (pixel = y*w + x, sample, vertex | stream << 31, seed). */
@@ -110,13 +118,19 @@ typedef struct spt_params {
 typedef struct spt_stats {
   uint64_t samples;        /* pixel-samples finished = camera rays */
   uint64_t path_rays;      /* rays traced through the scene for path vertices (incl. camera rays) */
-  uint64_t shadow_rays;    /* NEE shadow rays traced */
+  uint64_t shadow_rays;    /* NEE shadow rays of the reference: one per NEE event (:466). The kernel
+                              traces only `shadow_traced` of them (below); the others cannot reach
+                              the light and are rejected exactly by the light's own test */
   uint64_t vertices;       /* path vertices shaded (incl. terminal ones) */
   uint64_t nee_events;     /* NEE light samples taken (:465) */
   uint64_t nee_light_hits; /* ... whose shadow ray hit light_id (:470-472) */
   uint64_t cosine_samples; /* cosine-weighted scatter directions drawn (:337-347) */
   uint64_t misses;         /* path rays that hit nothing (reference: x = origin, id = 0, :373-374) */
-  double flop;             /* algorithmic FLOPs (model in spt_flops.h) */
+  uint64_t shadow_traced;  /* NEE shadow rays actually traced through the scene by the kernel */
+  uint64_t sphere_vertices;/* vertices on a sphere (Sphere::normal :246-253) */
+  double flop;             /* algorithmic FLOPs of the reference's work (model in spt_flops.h): every
+                              shadow ray of :466 charged as a full scene test */
+  double flop_executed;    /* the same model with only the traced shadow rays charged */
   double kernel_ms;        /* device time of the render kernel (HIP events) */
 } spt_stats;
 
@@ -134,11 +148,15 @@ spt_status spt_scene_cornell_specular(spt_prim* out, int32_t cap, int32_t* n_out
 /* The classic smallpt sphere box of the reference's older revision (the constants mined from the
  * shipped src/a.exe; its renders are the repository's image*.ppm): walls are
  * spheres of radius 1e5 (left x = 1e5+1 green, right x = -1e5+99 red, back, front (black), floor,
- * ceiling y = -1e5+81.6), a mirror and a glass ball of radius 16.5 at (27,16.5,47) / (73,16.5,78),
- * and the light, a sphere of radius 600 at (50, 681.33, 81.6) with emission 12 (prim 8). 9 prims.
- * Spheres of radius >= SPT_WIDE_SPHERE_RADIUS are intersected in fp64 (an fp32 quadratic cannot
- * hold a 1e5 wall to the scene's scale). */
+ * ceiling y = -1e5+81.6), two matte white (DIFF, .999) balls of radius 16.5 at (27,16.5,47) /
+ * (73,16.5,78), and the light, a sphere of radius 600 at (50, 681.33, 81.6) with emission 12
+ * (prim 8). 9 prims. Spheres of radius >= SPT_WIDE_SPHERE_RADIUS are intersected in fp64 (an fp32
+ * quadratic cannot hold a 1e5 wall to the scene's scale). NEE (nee_prob > 0) samples the light
+ * RECTANGLE of spt_params, which this scene does not have: render it with nee_prob = 0. */
 spt_status spt_scene_smallpt_classic(spt_prim* out, int32_t cap, int32_t* n_out);
+/* The same box with smallpt's original materials: the left ball a mirror (SPEC), the right one
+ * glass (REFR; shading = the commented-out code :481-495). 9 prims. */
+spt_status spt_scene_smallpt_mirror_glass(spt_prim* out, int32_t cap, int32_t* n_out);
 #define SPT_WIDE_SPHERE_RADIUS 1000.0
 /* Rows rendered by this shard (params tile_rows/shard_index/shard_count), ascending. Returns count. */
 int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
@@ -162,6 +180,37 @@ spt_status spt_render_async(spt_context* ctx, const spt_prim* prims, int32_t n_p
                             void* stream);
 /* Synchronises the context's last render and returns its stats. */
 spt_status spt_context_stats(spt_context* ctx, spt_stats* out);
+
+/* ---- multi-GPU: row-tile shards and ONE framebuffer gather over RCCL ----
+ * The reference's only parallel construct is the OpenMP pragma over its row loop (:526-528). Here
+ * rows are sharded in tiles of tile_rows across ranks (tile t -> rank t % n, spt_shard_rows);
+ * every rank renders its rows with spt_render_async into a compact buffer, and rank 0 receives
+ * all of them in one grouped ncclSend/ncclRecv over xGMI and de-interleaves the tiles into the
+ * image (h*w*3 floats). The image is bit-identical for any rank count. */
+#define SPT_COMM_ID_BYTES 128
+typedef struct spt_comm spt_comm;
+/* One process per GPU: rank 0 creates the id and the caller hands it to every rank (any channel). */
+spt_status spt_comm_unique_id(uint8_t id[SPT_COMM_ID_BYTES]);
+spt_status spt_comm_create(const uint8_t id[SPT_COMM_ID_BYTES], int32_t nranks, int32_t rank,
+                           int32_t device, spt_comm** out);
+spt_status spt_comm_destroy(spt_comm* comm);
+/* Allocate rank 0's receive slots for renders of this size ahead of a timed loop (optional). */
+spt_status spt_comm_reserve(spt_comm* comm, const spt_params* p);
+/* The gather, enqueued on `stream` after this rank's render: shard_dev = the rank's compact rows
+ * (spt_render_async's output for p with shard_index = rank), image_dev = the full image on rank 0
+ * (ignored elsewhere). p->shard_count must equal nranks. No host synchronisation. */
+spt_status spt_gather_framebuffer(spt_comm* comm, const spt_params* p, const float* shard_dev,
+                                  float* image_dev, void* stream);
+/* The de-interleave alone (rank 0's last step): shards_dev[k] = shard k's compact rows (device
+ * pointers on the current device), image_dev = h*w*3 floats. */
+spt_status spt_deinterleave_rows(const spt_params* p, int32_t nranks, const float* const* shards_dev,
+                                 float* image_dev, void* stream);
+/* One process driving n_dev GPUs (smallpt_amd --devices N): shard k renders on devices[k]
+ * (distinct), the gather lands on devices[0], rgb_out = the full image on the host (h*w*3 floats).
+ * p's shard fields are ignored. stats: summed over devices, kernel_ms = the slowest device's. */
+spt_status spt_render_multi(const spt_prim* prims, int32_t n_prims, const spt_camera* cam,
+                            const spt_params* p, const int32_t* devices, int32_t n_dev,
+                            float* rgb_out, spt_stats* stats);
 
 /* ---- image output (:313-321 toInt/clamp, :548-551 the P3 writer) ----
  * The encoder turns a DEVICE framebuffer (h*w*3 floats, row-major, y=0 top: what spt_render_async

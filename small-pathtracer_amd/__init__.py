@@ -36,7 +36,7 @@ LIGHT_GLIBC_WRAP, LIGHT_UNIFORM = 0, 1
 PHILOX_KEY1 = 0x53505431
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "no usable gfx950 device",
-          4: "device out of memory", 5: "unsupported feature"}
+          4: "device out of memory", 5: "unsupported feature", 6: "RCCL error"}
 
 
 class SptError(RuntimeError):
@@ -78,24 +78,36 @@ class spt_stats(ctypes.Structure):
                 ("shadow_rays", ctypes.c_uint64), ("vertices", ctypes.c_uint64),
                 ("nee_events", ctypes.c_uint64), ("nee_light_hits", ctypes.c_uint64),
                 ("cosine_samples", ctypes.c_uint64), ("misses", ctypes.c_uint64),
-                ("flop", ctypes.c_double), ("kernel_ms", ctypes.c_double)]
+                ("shadow_traced", ctypes.c_uint64), ("sphere_vertices", ctypes.c_uint64),
+                ("flop", ctypes.c_double), ("flop_executed", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 STAT_KEYS = ["samples", "path_rays", "shadow_rays", "vertices", "nee_events", "nee_light_hits",
-             "cosine_samples", "misses"]
+             "cosine_samples", "misses", "shadow_traced", "sphere_vertices"]
 
 # Every entry point declared in include/spt.h (checked by tests/test_capi.py).
 EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_scene_spheres32",
-           "spt_scene_cornell_specular", "spt_scene_smallpt_classic",
+           "spt_scene_cornell_specular", "spt_scene_smallpt_classic", "spt_scene_smallpt_mirror_glass",
            "spt_shard_rows", "spt_render", "spt_context_create", "spt_context_destroy",
            "spt_context_reserve", "spt_render_async", "spt_context_stats", "spt_abi_version",
            "spt_status_string", "spt_last_error", "spt_device_count", "spt_image_bound",
-           "spt_encoder_create", "spt_encoder_destroy", "spt_encode_image", "spt_write_image"]
+           "spt_encoder_create", "spt_encoder_destroy", "spt_encode_image", "spt_write_image",
+           "spt_comm_unique_id", "spt_comm_create", "spt_comm_destroy", "spt_comm_reserve",
+           "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi"]
 IMAGE_FORMATS = {"p3": 0, "p6": 1, "pfm": 2}
 FLAG_UNIFORM_SCATTER = 1  # spt_params.flags: random_scattering from the uniform code of :352-359
+# spt_params.flags bits 8-9: cap on the kernel specialisation (A/B and tests; never changes results).
+# "head"/"auto": the most specialised kernel the host can prove applicable.
+KERNEL_LEVELS = {"auto": 0, "head": 0, "generic": 1, "cornell": 2, "const": 3}
+
+
+def kernel_flag(name: str) -> int:
+    """spt_params.flags bits selecting the kernel specialisation cap `name` (KERNEL_LEVELS)."""
+    return KERNEL_LEVELS[name] << 8
 
 _lib = None
 
@@ -124,6 +136,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.spt_scene_spheres32.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_scene_cornell_specular.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_scene_smallpt_classic.argtypes = [P(spt_prim), I32, P(I32)]
+    lib.spt_scene_smallpt_mirror_glass.argtypes = [P(spt_prim), I32, P(I32)]
     lib.spt_shard_rows.argtypes = [P(spt_params), P(I32), I32]
     lib.spt_shard_rows.restype = I32
     lib.spt_render.argtypes = [P(spt_prim), I32, P(spt_camera), P(spt_params),
@@ -150,8 +163,21 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     for name in ("spt_encoder_create", "spt_encoder_destroy", "spt_encode_image",
                  "spt_write_image"):
         getattr(lib, name).restype = I32
+    VP = ctypes.c_void_p
+    lib.spt_comm_unique_id.argtypes = [P(ctypes.c_uint8)]
+    lib.spt_comm_create.argtypes = [P(ctypes.c_uint8), I32, I32, I32, P(VP)]
+    lib.spt_comm_destroy.argtypes = [VP]
+    lib.spt_comm_reserve.argtypes = [VP, P(spt_params)]
+    lib.spt_gather_framebuffer.argtypes = [VP, P(spt_params), VP, VP, VP]
+    lib.spt_deinterleave_rows.argtypes = [P(spt_params), I32, P(VP), VP, VP]
+    lib.spt_render_multi.argtypes = [P(spt_prim), I32, P(spt_camera), P(spt_params), P(I32), I32,
+                                     P(ctypes.c_float), P(spt_stats)]
+    for name in ("spt_comm_unique_id", "spt_comm_create", "spt_comm_destroy", "spt_comm_reserve",
+                 "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi"):
+        getattr(lib, name).restype = I32
     for name in ("spt_default_params", "spt_camera_init", "spt_scene_cornell",
                  "spt_scene_spheres32", "spt_scene_cornell_specular", "spt_scene_smallpt_classic",
+                 "spt_scene_smallpt_mirror_glass",
                  "spt_render", "spt_context_create",
                  "spt_context_destroy", "spt_context_reserve", "spt_render_async",
                  "spt_context_stats"):
@@ -264,11 +290,22 @@ def cornell_scene() -> list:
 
 def smallpt_classic_scene() -> list:
     """spt_scene_smallpt_classic(): the classic smallpt sphere box of the reference's older revision
-    (walls of radius 1e5, fp64-tested; mirror, glass and the radius-600 light sphere, prim 8)."""
+    and its shipped image*.ppm (walls of radius 1e5, fp64-tested; two matte white balls; the
+    radius-600 light sphere, prim 8). Render with nee_prob = 0 (no light rectangle)."""
     lib = load_library()
     arr = (spt_prim * 16)()
     n = ctypes.c_int32()
     _check(lib.spt_scene_smallpt_classic(arr, 16, ctypes.byref(n)))
+    return [arr[i] for i in range(n.value)]
+
+
+def smallpt_mirror_glass_scene() -> list:
+    """spt_scene_smallpt_mirror_glass(): the same box with smallpt's mirror (SPEC) and glass (REFR)
+    balls."""
+    lib = load_library()
+    arr = (spt_prim * 16)()
+    n = ctypes.c_int32()
+    _check(lib.spt_scene_smallpt_mirror_glass(arr, 16, ctypes.byref(n)))
     return [arr[i] for i in range(n.value)]
 
 
@@ -364,6 +401,72 @@ class Renderer:
         return st.as_dict()
 
 
+def render_multi(prims: Sequence[spt_prim], cam: Camera, params: spt_params, devices,
+                 return_stats=False):
+    """One process, len(devices) GPUs (spt_render_multi): shard k on devices[k], one RCCL gather to
+    devices[0]. Returns the full (h, w, 3) image, bit-identical to render() on one GPU."""
+    lib = load_library()
+    devs = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+    out = np.empty((params.height, params.width, 3), dtype=np.float32)
+    st = spt_stats()
+    _check(lib.spt_render_multi(_scene_array(prims), len(prims), ctypes.byref(cam._c),
+                                ctypes.byref(params), devs, len(devices),
+                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                ctypes.byref(st)))
+    return (out, st.as_dict()) if return_stats else out
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """spt_comm_unique_id(): the RCCL unique id rank 0 hands to every rank."""
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    _check(load_library().spt_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """One rank of the framebuffer gather (spt_comm_*): RCCL over xGMI, rank 0 receives."""
+
+    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int):
+        self.lib = load_library()
+        self._c = ctypes.c_void_p()
+        idb = (ctypes.c_uint8 * COMM_ID_BYTES)(*unique_id)
+        _check(self.lib.spt_comm_create(idb, int(nranks), int(rank), int(device),
+                                        ctypes.byref(self._c)))
+        self.nranks, self.rank, self.device = nranks, rank, device
+
+    def close(self):
+        if self._c:
+            self.lib.spt_comm_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def reserve(self, params: spt_params):
+        _check(self.lib.spt_comm_reserve(self._c, ctypes.byref(params)))
+
+    def gather(self, params: spt_params, shard_dev_ptr: int, image_dev_ptr: int, stream_ptr: int = 0):
+        """Enqueue the gather of this rank's shard (rank 0: into image_dev_ptr) on the stream."""
+        _check(self.lib.spt_gather_framebuffer(self._c, ctypes.byref(params),
+                                               ctypes.c_void_p(shard_dev_ptr),
+                                               ctypes.c_void_p(image_dev_ptr or None),
+                                               ctypes.c_void_p(stream_ptr or None)))
+
+
+def deinterleave_rows(params: spt_params, shard_dev_ptrs, image_dev_ptr: int, stream_ptr: int = 0):
+    """spt_deinterleave_rows(): shard k's compact rows (device pointers) -> the image."""
+    arr = (ctypes.c_void_p * len(shard_dev_ptrs))(*[ctypes.c_void_p(int(x)) for x in shard_dev_ptrs])
+    _check(load_library().spt_deinterleave_rows(ctypes.byref(params), len(shard_dev_ptrs), arr,
+                                                ctypes.c_void_p(image_dev_ptr),
+                                                ctypes.c_void_p(stream_ptr or None)))
+
+
 # ---------------------------------------------------------------------------------------------
 # Output (:313-321 toInt/clamp, :548-551 the P3 writer): encoded on the GPU (spt_image.hip)
 # ---------------------------------------------------------------------------------------------
@@ -408,11 +511,14 @@ class Encoder:
         return int(n.value)
 
 
-def flop_model(stats: dict, prims: Iterable[spt_prim]) -> float:
-    """include/spt_flops.h model (same as the C side)."""
+def flop_model(stats: dict, prims: Iterable[spt_prim], executed: bool = False) -> float:
+    """include/spt_flops.h model (same as the C side): `flop`, or with executed=True
+    `flop_executed` (only the traced shadow rays charged a scene test)."""
     scene = sum(19 if p.kind == SPHERE else 6 for p in prims)
-    return (stats["samples"] * 40 + (stats["path_rays"] + stats["shadow_rays"]) * scene
-            + stats["vertices"] * 11 + (stats["vertices"] - stats["samples"]) * 12
+    shadow = stats["shadow_traced"] if executed else stats["shadow_rays"]
+    return (stats["samples"] * 40 + (stats["path_rays"] + shadow) * scene
+            + stats["vertices"] * 11 + stats["sphere_vertices"] * 13
+            + (stats["vertices"] - stats["samples"]) * 12
             + stats["cosine_samples"] * 65 + stats["nee_events"] * 19
             + stats["nee_light_hits"] * 14)
 

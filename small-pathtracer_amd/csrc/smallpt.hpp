@@ -116,6 +116,24 @@ inline std::vector<spt_prim> smallpt_classic_scene() {
   return s;
 }
 
+// The same box with smallpt's mirror (SPEC) and glass (REFR) balls.
+inline std::vector<spt_prim> smallpt_mirror_glass_scene() {
+  std::vector<spt_prim> s(9);
+  int32_t n = 0;
+  spt_scene_smallpt_mirror_glass(s.data(), 9, &n);
+  s.resize(n);
+  return s;
+}
+
+// Config 5's 32-sphere scene (spt_scene_spheres32).
+inline std::vector<spt_prim> spheres32_scene() {
+  std::vector<spt_prim> s(64);
+  int32_t n = 0;
+  spt_scene_spheres32(s.data(), 64, &n);
+  s.resize(n);
+  return s;
+}
+
 inline double clamp(double x) { return x < 0 ? 0 : x > 1 ? 1 : x; }                 // :314-316
 inline int toInt(double x) { return int(std::pow(clamp(x), 1 / 2.2) * 255 + .5); }  // :319-321
 
@@ -132,6 +150,19 @@ inline std::vector<float> render(const std::vector<spt_prim>& scene, const Camer
                                  const spt_params& p, spt_stats* stats = nullptr) {
   std::vector<float> c(3ull * (size_t)spt_shard_rows(&p, nullptr, 0) * (size_t)p.width);
   const spt_status s = spt_render(scene.data(), (int32_t)scene.size(), &cam.abi(), &p, c.data(), stats);
+  if (s != SPT_OK)
+    throw std::runtime_error(std::string(spt_status_string(s)) + ": " + spt_last_error());
+  return c;
+}
+
+// The same drop-in on several GPUs of one process: row tiles sharded over `devices`, one RCCL
+// gather to devices[0] (spt_render_multi). Bit-identical to render().
+inline std::vector<float> render_multi(const std::vector<spt_prim>& scene, const Camera& cam,
+                                       const spt_params& p, const std::vector<int32_t>& devices,
+                                       spt_stats* stats = nullptr) {
+  std::vector<float> c(3ull * (size_t)p.height * (size_t)p.width);
+  const spt_status s = spt_render_multi(scene.data(), (int32_t)scene.size(), &cam.abi(), &p,
+                                        devices.data(), (int32_t)devices.size(), c.data(), stats);
   if (s != SPT_OK)
     throw std::runtime_error(std::string(spt_status_string(s)) + ": " + spt_last_error());
   return c;

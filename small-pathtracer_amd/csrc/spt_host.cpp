@@ -147,9 +147,13 @@ extern "C" spt_status spt_scene_cornell_specular(spt_prim* o, int32_t cap, int32
   return SPT_OK;
 }
 
-extern "C" spt_status spt_scene_smallpt_classic(spt_prim* o, int32_t cap, int32_t* n_out) {
+// The classic smallpt sphere box. The shipped image*.ppm of the reference's
+// older revision show its two r = 16.5 balls as matte white DIFF spheres (colour .999, the .rdata
+// constant); `mirror_glass` gives them smallpt's original SPEC / REFR materials instead.
+static spt_status classic_box(spt_prim* o, int32_t cap, int32_t* n_out, bool mirror_glass) {
   if (!o || !n_out || cap < 9) return SPT_ERR_INVALID_ARG;
   struct S { double r, x, y, z, e, c0, c1, c2; int refl; };
+  const int ball0 = mirror_glass ? SPT_SPEC : SPT_DIFF, ball1 = mirror_glass ? SPT_REFR : SPT_DIFF;
   const S sc[9] = {
       {1e5, 1e5 + 1, 40.8, 81.6, 0, .25, .75, .25, SPT_DIFF},   // left (green)
       {1e5, -1e5 + 99, 40.8, 81.6, 0, .75, .25, .25, SPT_DIFF}, // right (red)
@@ -157,8 +161,8 @@ extern "C" spt_status spt_scene_smallpt_classic(spt_prim* o, int32_t cap, int32_
       {1e5, 50, 40.8, -1e5 + 170, 0, 0, 0, 0, SPT_DIFF},        // front
       {1e5, 50, 1e5, 81.6, 0, .75, .75, .75, SPT_DIFF},         // floor
       {1e5, 50, -1e5 + 81.6, 81.6, 0, .75, .75, .75, SPT_DIFF}, // ceiling
-      {16.5, 27, 16.5, 47, 0, .999, .999, .999, SPT_SPEC},      // mirror
-      {16.5, 73, 16.5, 78, 0, .999, .999, .999, SPT_REFR},      // glass
+      {16.5, 27, 16.5, 47, 0, .999, .999, .999, ball0},         // left ball (smallpt: mirror)
+      {16.5, 73, 16.5, 78, 0, .999, .999, .999, ball1},         // right ball (smallpt: glass)
       {600, 50, 681.6 - .27, 81.6, 12, 0, 0, 0, SPT_DIFF}};     // light
   for (int k = 0; k < 9; ++k) {
     spt_prim* p = &o[k];
@@ -172,6 +176,14 @@ extern "C" spt_status spt_scene_smallpt_classic(spt_prim* o, int32_t cap, int32_
   }
   *n_out = 9;
   return SPT_OK;
+}
+
+extern "C" spt_status spt_scene_smallpt_classic(spt_prim* o, int32_t cap, int32_t* n_out) {
+  return classic_box(o, cap, n_out, false);
+}
+
+extern "C" spt_status spt_scene_smallpt_mirror_glass(spt_prim* o, int32_t cap, int32_t* n_out) {
+  return classic_box(o, cap, n_out, true);
 }
 
 // Row-tile sharding: tile t (rows [t*T, t*T+T)) belongs to shard t % shard_count; a shard's rows
@@ -201,6 +213,7 @@ extern "C" const char* spt_status_string(spt_status s) {
     case SPT_ERR_NO_DEVICE: return "no usable gfx950 device";
     case SPT_ERR_OOM: return "device out of memory";
     case SPT_ERR_UNSUPPORTED: return "unsupported feature";
+    case SPT_ERR_RCCL: return "RCCL error";
   }
   return "unknown status";
 }

@@ -46,7 +46,10 @@ constexpr uint32_t kStShadow = 5;  // a NEE shadow ray toward the light is set: 
 constexpr uint32_t kStTerm = 6;    // the path ended at this vertex (within an iteration)
 // Exit condition every wave reaches even if a path never terminated: a C3 wave runs ~4e3
 // iterations and a 1-GPU C5 wave ~3e6; stats[0] counts waves that hit the cap.
-constexpr uint32_t kMaxWaveIters = 1u << 26;  // [0,8) path stats, [8,28) region stats (diagnostic build)
+constexpr uint32_t kMaxWaveIters = 1u << 26;
+// stats[]: [0] waves that hit kMaxWaveIters, [1,8) path statistics (spt_stats order), [8] shadow
+// rays traced, [9] sphere vertices, [12,32) region stats (diagnostic build)
+[[maybe_unused]] constexpr int kStatShadowTraced = 8, kStatSphereVertices = 9, kStatRegion = 12;
 
 // 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
 // axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
@@ -551,7 +554,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
   uint32_t n_path = 0, n_cos = 0;
   // Per-lane counts of events that happen inside divergent blocks, incremented in place and
   // summed once at the end (a boolean per event carried to a convergent ballot cost 3 VALU each).
+  // NEE events need no counter in the HEAD NEE kernels: with NEE always on and no SPEC/REFR, every
+  // non-terminal vertex takes one (nee_events = vertices - samples, added by the host).
+  constexpr bool kNeeByIdentity = CF::NEE == 1 && !TP::MAT;
   uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
+  uint32_t l_shadow = 0;  // shadow rays traced (NEE samples that passed light_accepts())
+  uint32_t l_sph = 0;     // vertices on a sphere (their normal is the FLOP model's sphere term)
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
   uint32_t reg_flags = 0;
@@ -696,6 +704,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
         const bool lh = id == light_id_of<CF>(D);
         if (lh) SPT_REGION(7);
         l_hit += lh ? 1u : 0u;
+        ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
         const float pdf = fabsf(div_mk(larea * d.y, t * t));            // :471
         const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
@@ -755,6 +764,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
           const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
           if (TP::MAT) gn = n;
+          ++l_sph;
         }
         }
         f3 f = mk(H.cx, H.cy, H.cz);
@@ -860,7 +870,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
             }
             const float ly = CF::LREF == 1 ? kRefLy : D->ly;
             const f3 dl = normalize3(mk(xl - x.x, ly - x.y, zl - x.z));
-            l_nee += term ? 0u : 1u;
+            if constexpr (!kNeeByIdentity) l_nee += term ? 0u : 1u;
             const SPT_CONST SceneGeo* G2 = TP::CONSTGEO ? nullptr : cptr(D->geo);
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
             const bool la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
@@ -925,8 +935,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
 #ifdef SPT_REGION_STATS
     if (lane == 0) {  // wave-uniform values: one lane adds them
       for (int k = 0; k < kRegions; ++k) {
-        atomicAdd(st + 8 + 2 * k, (unsigned long long)reg_exec[k]);
-        atomicAdd(st + 9 + 2 * k, (unsigned long long)reg_lanes[k]);
+        atomicAdd(st + kStatRegion + 2 * k, (unsigned long long)reg_exec[k]);
+        atomicAdd(st + kStatRegion + 1 + 2 * k, (unsigned long long)reg_lanes[k]);
       }
     }
 #endif
@@ -944,11 +954,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams* __restric
       atomicAdd(st + 3, samples);
     }
     {  // per-lane event counts (the atomic optimizer reduces each over the wave)
-      atomicAdd(st + 2, (unsigned long long)l_nee);
+      if constexpr (!kNeeByIdentity) {
+        atomicAdd(st + 2, (unsigned long long)l_nee);
+        atomicAdd(st + 4, (unsigned long long)l_nee);
+      }
       atomicAdd(st + 3, (unsigned long long)l_hit);
-      atomicAdd(st + 4, (unsigned long long)l_nee);
       atomicAdd(st + 5, (unsigned long long)l_hit);
       atomicAdd(st + 7, (unsigned long long)l_miss);
+      atomicAdd(st + kStatShadowTraced, (unsigned long long)l_shadow);
+      if constexpr (TP::SPH) atomicAdd(st + kStatSphereVertices, (unsigned long long)l_sph);
     }
   }
 }
@@ -983,7 +997,8 @@ static spt_status fail(spt_status s, const std::string& msg) {
                   std::string(#call) + ": " + hipGetErrorString(e_));                    \
   } while (0)
 
-// Kernel variants, from the most general to the most specialised (SPT_KERNEL caps the level).
+// Kernel variants, from the most general to the most specialised (SPT_FLAG_KERNEL_LEVEL caps the
+// level).
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
@@ -1012,6 +1027,7 @@ struct spt_context {
   KParams* d_kp = nullptr;   // kernel parameters in device memory (read via s_load)
   KParams* h_kp = nullptr;   // pinned staging
   uint64_t samples = 0;      // pixel-samples of the last render (exact, not counted in-kernel)
+  bool nee_by_identity = false;  // the last kernel derives nee_events from vertices - samples
   double scene_flop = 0;     // FLOP-model cost of one ray against the scene
 };
 
@@ -1029,7 +1045,10 @@ static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* c
   if (p->shard_count < 1 || p->shard_index < 0 || p->shard_index >= p->shard_count)
     return fail(SPT_ERR_INVALID_ARG, "bad shard_index/shard_count");
   if (p->tile_rows < 0 || p->chunk < 0) return fail(SPT_ERR_INVALID_ARG, "negative tile/chunk");
-  if (p->flags & ~SPT_FLAG_UNIFORM_SCATTER) return fail(SPT_ERR_INVALID_ARG, "unknown flags");
+  if (p->flags & ~(SPT_FLAG_UNIFORM_SCATTER | SPT_FLAG_KERNEL_LEVEL_MASK))
+    return fail(SPT_ERR_INVALID_ARG, "unknown flags");
+  if (((p->flags & SPT_FLAG_KERNEL_LEVEL_MASK) >> 8) > SPT_KERNEL_LEVEL_CONST)
+    return fail(SPT_ERR_INVALID_ARG, "bad kernel level");
   if (p->light_mode != SPT_LIGHT_GLIBC_WRAP && p->light_mode != SPT_LIGHT_UNIFORM)
     return fail(SPT_ERR_INVALID_ARG, "bad light_mode");
   if (p->light_mode == SPT_LIGHT_GLIBC_WRAP &&
@@ -1040,6 +1059,16 @@ static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* c
       return fail(SPT_ERR_INVALID_ARG, "bad primitive kind");
     if (prims[i].refl < SPT_DIFF || prims[i].refl > SPT_REFR)
       return fail(SPT_ERR_INVALID_ARG, "bad material");
+  }
+  // NEE (:464-472) weights shadow rays that reach prims[light_id] as light hits: that primitive
+  // must exist and emit, or the image is silently wrong (e.g. the classic sphere box with the HEAD
+  // light id 6, a ball).
+  if (p->nee_prob > 0.0f) {
+    if (p->light_id < 0 || p->light_id >= n)
+      return fail(SPT_ERR_INVALID_ARG, "nee_prob > 0 needs light_id in [0, n_prims)");
+    const double* e = prims[p->light_id].e;
+    if (!(e[0] != 0.0 || e[1] != 0.0 || e[2] != 0.0))
+      return fail(SPT_ERR_INVALID_ARG, "nee_prob > 0 but prims[light_id] emits nothing");
   }
   return SPT_OK;
 }
@@ -1281,6 +1310,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const int rows = spt_shard_row_count(p);
   if (rows == 0) {  // a shard that owns no rows (more shards than row tiles): nothing to render
     c->samples = 0;
+    c->nee_by_identity = false;
     c->scene_flop = 0;
     SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
     SPT_HIP(hipEventRecord(c->ev0, stream));
@@ -1289,12 +1319,48 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     return SPT_OK;
   }
   K.n_local_pix = rows * p->width;
+  K.light_black = light_pos >= 0 && c->h_prims[p->light_id].pmax == 0.0f ? 1 : 0;
+  // Topology specialisation: the HEAD Cornell box (6 XY, 5 XZ, 6 YZ rects, light at grouped
+  // position 8) runs a fully unrolled intersect; anything else the generic loops.
+  const SceneGeo& g = *c->h_geo;
+  bool all_diff = true;
+  for (int i = 0; i < n_prims; ++i) all_diff = all_diff && prims[i].refl == SPT_DIFF;
+  // The HEAD-topology kernels are all-DIFF, cosine-scatter specialisations; anything else (SPEC/
+  // REFR, the uniform hemisphere) runs the generic kernel.
+  // spt_params.flags SPT_FLAG_KERNEL_LEVEL (A/B and tests; never changes results): cap the
+  // specialisation level. 0 = auto (the most specialised kernel the host can prove).
+  const uint32_t klevel = (p->flags & SPT_FLAG_KERNEL_LEVEL_MASK) >> 8;
+  const int kcap = klevel == SPT_KERNEL_LEVEL_GENERIC   ? 0
+                   : klevel == SPT_KERNEL_LEVEL_CORNELL ? 1
+                   : klevel == SPT_KERNEL_LEVEL_CONST   ? 2
+                                                        : 3;
+  const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
+                       g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8 &&
+                       g.n_txy == 3 && g.n_txz == 4 && g.n_tyz == 3;
+  const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
+  // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
+  // axis-aligned camera (Cfg CAMAX): horizontal.y/z and vertical.x/z zero, origin nonzero
+  bool cam_axis = K.cam[7] == 0.0f && K.cam[8] == 0.0f && K.cam[9] == 0.0f && K.cam[11] == 0.0f &&
+                  K.cam[0] != 0.0f && K.cam[1] != 0.0f && K.cam[2] != 0.0f;
+  for (int i = 0; i < 12; ++i) cam_axis = cam_axis && std::isfinite(K.cam[i]);
+  const bool lref = p->rr_depth == kRefRrDepth && p->light_id == kRefLightId &&
+                    p->light_x0 == kRefLx0 && p->light_dx == 36.0f && p->light_z0 == kRefLz0 &&
+                    p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
+  const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
+                        p->rr_depth >= 1 && cam_axis && lref;
+  int kv = g.n_sph_wide > 0 ? KV_WIDE : KV_GENERIC;  // (only the wide kernel has the fp64 loop)
+  if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
+  else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
+  else if (cconst) kv = KV_CONST;
+  else if (cornell) kv = KV_CORNELL;
+  else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
+    kv = KV_SPHDIFF;
   // Unit size: ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured
   // 25.0 ms vs 26.0 ms at 8 units/lane and 27.8 ms at 2); never changes results (integer
   // accumulation).
   int chunk = p->chunk;
   if (chunk <= 0) {
-    const double lanes = (double)c->n_cu * c->blocks_per_cu * kBlock;
+    const double lanes = (double)c->n_cu * c->bpc[kv] * kBlock;  // resident lanes of THIS kernel
     const double want_units = 16.0 * lanes;
     const double per_pix = std::max(1.0, want_units / std::max(1, K.n_local_pix));
     chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
@@ -1321,7 +1387,6 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.accum = c->accum;
   K.queue = c->queue;
   K.stats = c->stats;
-  K.light_black = light_pos >= 0 && c->h_prims[p->light_id].pmax == 0.0f ? 1 : 0;
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
   K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
@@ -1338,41 +1403,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                          stream));
   SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream));
   SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
-  // Topology specialisation: the HEAD Cornell box (6 XY, 5 XZ, 6 YZ rects, light at grouped
-  // position 8) runs a fully unrolled intersect; anything else the generic loops.
-  const SceneGeo& g = *c->h_geo;
-  bool all_diff = true;
-  for (int i = 0; i < n_prims; ++i) all_diff = all_diff && prims[i].refl == SPT_DIFF;
-  // The HEAD-topology kernels are all-DIFF, cosine-scatter specialisations; anything else (SPEC/
-  // REFR, the uniform hemisphere) runs the generic kernel.
-  // SPT_KERNEL=generic|cornell|const|head (A/B and tests): cap the specialisation level.
-  const char* kenv = std::getenv("SPT_KERNEL");
-  const int kcap = !kenv                               ? 3
-                   : std::strcmp(kenv, "generic") == 0 ? 0
-                   : std::strcmp(kenv, "cornell") == 0 ? 1
-                   : std::strcmp(kenv, "const") == 0   ? 2
-                                                       : 3;
-  const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
-                       g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8 &&
-                       g.n_txy == 3 && g.n_txz == 4 && g.n_tyz == 3;
-  const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
-  // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
-  // axis-aligned camera (Cfg CAMAX): horizontal.y/z and vertical.x/z zero, origin nonzero
-  bool cam_axis = K.cam[7] == 0.0f && K.cam[8] == 0.0f && K.cam[9] == 0.0f && K.cam[11] == 0.0f &&
-                  K.cam[0] != 0.0f && K.cam[1] != 0.0f && K.cam[2] != 0.0f;
-  for (int i = 0; i < 12; ++i) cam_axis = cam_axis && std::isfinite(K.cam[i]);
-  const bool lref = p->rr_depth == kRefRrDepth && p->light_id == kRefLightId &&
-                    p->light_x0 == kRefLx0 && p->light_dx == 36.0f && p->light_z0 == kRefLz0 &&
-                    p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
-  const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
-                        p->rr_depth >= 1 && cam_axis && lref;
-  int kv = g.n_sph_wide > 0 ? KV_WIDE : KV_GENERIC;  // (only the wide kernel has the fp64 loop)
-  if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
-  else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
-  else if (cconst) kv = KV_CONST;
-  else if (cornell) kv = KV_CORNELL;
-  else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
-    kv = KV_SPHDIFF;
+  c->nee_by_identity = kv == KV_CONST_NEE;
   const int grid = c->n_cu * c->bpc[kv];
   SPT_HIP(hipEventRecord(c->ev0, stream));
   hipLaunchKernelGGL(kRenderKernels[kv], dim3(grid), dim3(kBlock), 0, stream,
@@ -1400,7 +1431,8 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
                                     "path_end"};
     std::fprintf(stderr, "SPT_REGION_STATS");
     for (int r = 0; r < 10; ++r)
-      std::fprintf(stderr, " %s=%llu/%llu", names[r], h[8 + 2 * r], h[9 + 2 * r]);
+      std::fprintf(stderr, " %s=%llu/%llu", names[r], h[kStatRegion + 2 * r],
+                   h[kStatRegion + 1 + 2 * r]);
     std::fprintf(stderr, "\n");
   }
 #endif
@@ -1415,14 +1447,25 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   out->samples = c->samples; out->path_rays = h[1]; out->shadow_rays = h[2]; out->vertices = h[3];
   out->nee_events = h[4]; out->nee_light_hits = h[5]; out->cosine_samples = h[6];
   out->misses = h[7];
-  // FLOP model (include/spt_flops.h): scene cost per ray from the primitive mix.
+  out->shadow_traced = h[kStatShadowTraced];
+  out->sphere_vertices = h[kStatSphereVertices];
+  if (c->nee_by_identity) {  // HEAD NEE kernels: one NEE event per non-terminal vertex
+    out->nee_events = out->vertices - out->samples;
+    out->shadow_rays = out->nee_events;
+  }
+  // FLOP model (include/spt_flops.h): scene cost per ray from the primitive mix. `flop` charges
+  // a full scene test for every shadow ray of the reference (:466); `flop_executed` only for the
+  // shadow rays the kernel traced (the others are rejected exactly by the light pre-test).
   const double scene = c->scene_flop;
-  out->flop = (double)out->samples * SPT_FLOP_SAMPLE +
-              (double)(out->path_rays + out->shadow_rays) * scene +
-              (double)out->vertices * SPT_FLOP_VERTEX +
-              (double)(out->vertices - out->samples) * SPT_FLOP_COMBINE +
-              (double)out->cosine_samples * SPT_FLOP_COSINE +
-              (double)out->nee_events * SPT_FLOP_NEE + (double)out->nee_light_hits * SPT_FLOP_NEE_HIT;
+  const double common = (double)out->samples * SPT_FLOP_SAMPLE +
+                        (double)out->path_rays * scene + (double)out->vertices * SPT_FLOP_VERTEX +
+                        (double)out->sphere_vertices * SPT_FLOP_SPHERE_NORMAL +
+                        (double)(out->vertices - out->samples) * SPT_FLOP_COMBINE +
+                        (double)out->cosine_samples * SPT_FLOP_COSINE +
+                        (double)out->nee_events * SPT_FLOP_NEE +
+                        (double)out->nee_light_hits * SPT_FLOP_NEE_HIT;
+  out->flop = common + (double)out->shadow_rays * scene;
+  out->flop_executed = common + (double)out->shadow_traced * scene;
   out->kernel_ms = ms;
   c->pending = false;
   return SPT_OK;

@@ -31,11 +31,12 @@ def test_exports_every_declared_symbol(spt):
 
 def test_abi_version_and_status_strings(spt):
     lib = spt.load_library()
-    assert lib.spt_abi_version() == 1
+    assert lib.spt_abi_version() == 2
     for code, text in spt.STATUS.items():
         assert lib.spt_status_string(code).decode() == text
 
 
+@pytest.mark.gpu
 def test_library_is_gfx950_code_object(spt):
     out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", spt.LIB_PATH], capture_output=True, text=True)
     if out.returncode != 0:
@@ -93,6 +94,36 @@ def test_invalid_arguments_fail_loudly(spt):
     with pytest.raises(spt.SptError) as e:
         spt.render(spt.cornell_scene(), cam, spt.default_params(width=8, height=8, spp=1, flags=4))
     assert e.value.status == 1
+
+
+def test_nee_needs_an_emitting_light(spt):
+    """NEE (nee_prob > 0) weights shadow rays reaching prims[light_id] as light hits: a light id
+    that is absent or does not emit is rejected (the classic box's HEAD id 6 is a ball there)."""
+    cam = spt.Camera(aspect=1.0)
+    classic = spt.smallpt_classic_scene()
+    for kw in (dict(), dict(light_id=40), dict(light_id=-1)):
+        with pytest.raises(spt.SptError) as e:
+            spt.render(classic, cam, spt.default_params(width=8, height=8, spp=1, **kw))
+        assert e.value.status == 1 and "light" in spt.load_library().spt_last_error().decode()
+
+
+def test_kernel_level_flag_is_validated(spt):
+    cam = spt.Camera(aspect=1.0)
+    with pytest.raises(spt.SptError) as e:  # bits 8-9 hold the level, bit 10 is not a flag
+        spt.render(spt.cornell_scene(), cam, spt.default_params(width=8, height=8, spp=1,
+                                                                flags=1 << 10))
+    assert e.value.status == 1
+    assert spt.kernel_flag("generic") == 1 << 8 and spt.kernel_flag("head") == 0
+
+
+def test_classic_scenes_differ_only_in_ball_materials(spt):
+    a, b = spt.smallpt_classic_scene(), spt.smallpt_mirror_glass_scene()
+    assert len(a) == len(b) == 9
+    assert [p.refl for p in a] == [0] * 9 and [p.refl for p in b] == [0] * 6 + [1, 2, 0]
+    for p, q in zip(a, b):
+        p.refl = q.refl = 0
+        assert bytes(p) == bytes(q)
+    assert a[8].e[0] == 12 and a[6].c[0] == .999
 
 
 def test_no_device_is_an_error_not_a_fallback(spt):
