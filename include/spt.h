@@ -150,14 +150,16 @@ spt_status spt_scene_cornell_specular(spt_prim* out, int32_t cap, int32_t* n_out
  * spheres of radius 1e5 (left x = 1e5+1 green, right x = -1e5+99 red, back, front (black), floor,
  * ceiling y = -1e5+81.6), two matte white (DIFF, .999) balls of radius 16.5 at (27,16.5,47) /
  * (73,16.5,78), and the light, a sphere of radius 600 at (50, 681.33, 81.6) with emission 12
- * (prim 8). 9 prims. Spheres of radius >= SPT_WIDE_SPHERE_RADIUS are intersected in fp64 (an fp32
- * quadratic cannot hold a 1e5 wall to the scene's scale). NEE (nee_prob > 0) samples the light
+ * (prim 8). 9 prims. Spheres of radius >= SPT_WIDE_SPHERE_RADIUS are intersected in fp64: an fp32
+ * quadratic cannot hold a 1e5 wall to the scene's scale, and for the radius-600 light, whose cap
+ * dips only 0.27 below the ceiling, r^2 - |q|^2 has an fp32 rounding step of ~0.03 (measured:
+ * concentric rings and a washed-out ceiling around the cap). NEE (nee_prob > 0) samples the light
  * RECTANGLE of spt_params, which this scene does not have: render it with nee_prob = 0. */
 spt_status spt_scene_smallpt_classic(spt_prim* out, int32_t cap, int32_t* n_out);
 /* The same box with smallpt's original materials: the left ball a mirror (SPEC), the right one
  * glass (REFR; shading = the commented-out code :481-495). 9 prims. */
 spt_status spt_scene_smallpt_mirror_glass(spt_prim* out, int32_t cap, int32_t* n_out);
-#define SPT_WIDE_SPHERE_RADIUS 1000.0
+#define SPT_WIDE_SPHERE_RADIUS 100.0 /* larger than the scenes' rooms (~100 units across) */
 /* Rows rendered by this shard (params tile_rows/shard_index/shard_count), ascending. Returns count. */
 int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
 

@@ -632,19 +632,23 @@ static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
  * nearer; the other one can only be the nearest hit of the two through the box's interior, i.e.
  * when the first plane's test is missed within an ulp of an edge. Every test then computes
  * t = n * inv_a exactly as a single rectangle (the same bits as testing that plane alone). */
-/* A wide sphere (the 1e5 walls of the classic smallpt box) in fp64: the cancellation-free
- * quadratic with explicit fma, IEEE sqrt, the fp32 contract's epsilon, t rounded to float. */
+/* A wide sphere (the 1e5 walls and the radius-600 light of the classic smallpt box) in fp64: the
+ * cancellation-free quadratic with explicit fma, IEEE division and sqrt, the fp32 contract's
+ * epsilon, t rounded to float. The quadratic keeps a = d.d (the fp32-normalised d is not exactly
+ * unit; assuming |d| = 1 puts an error (|d|^2 - 1) * b^2 ~ 1e3 into a radius-1e5 discriminant):
+ * t = k -+ sqrt(det / a), k = (op.d) / a, det = r^2 - |op - k d|^2. */
 static float c_sphere_wide(const c_prim* P, fv o, fv d) {
   const double ox = P->dpx - (double)o.x, oy = P->dpy - (double)o.y, oz = P->dpz - (double)o.z;
   const double dx = d.x, dy = d.y, dz = d.z;
-  const double bb = fma(oz, dz, fma(oy, dy, ox * dx));
-  const double qx = fma(-bb, dx, ox), qy = fma(-bb, dy, oy), qz = fma(-bb, dz, oz);
+  const double a = fma(dz, dz, fma(dy, dy, dx * dx));
+  const double k = fma(oz, dz, fma(oy, dy, ox * dx)) / a;
+  const double qx = fma(-k, dx, ox), qy = fma(-k, dy, oy), qz = fma(-k, dz, oz);
   const double det = P->drad2 - fma(qz, qz, fma(qy, qy, qx * qx));
   double sd, t1, t2;
   if (!(det >= 0.0)) return 0.0f;
-  sd = sqrt(det);
-  t1 = bb - sd;
-  t2 = bb + sd;
+  sd = sqrt(det / a);
+  t1 = k - sd;
+  t2 = k + sd;
   return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
 }
 

@@ -7,7 +7,7 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-c
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
-  /opt/rocm/bin/hipcc $FLAGS $defs -shared -o ../../build/ab/$name.so spt_kernel.hip spt_image.hip spt_host.cpp &
+  /opt/rocm/bin/hipcc $FLAGS $defs -shared -o ../../build/ab/$name.so spt_kernel.hip spt_image.hip spt_multi.hip spt_host.cpp -lrccl &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done

@@ -330,18 +330,22 @@ __device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d)
   return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
 }
 
-// A wide sphere (the 1e5 walls of the classic smallpt box) in fp64: the same cancellation-free
-// quadratic with explicit fma, an IEEE double sqrt, the fp32 contract's epsilon; t rounded to float
-// (oracle c_sphere_wide).
+// A wide sphere (the 1e5 walls and the radius-600 light of the classic smallpt box) in fp64: the
+// cancellation-free quadratic with explicit fma, IEEE double division and sqrt, the fp32 contract's
+// epsilon; t rounded to float (oracle c_sphere_wide). The fp32-normalised direction is not exactly
+// unit (|d|^2 = 1 + e, |e| ~ 1e-7), and a radius-1e5 quadratic that assumed |d| = 1 would carry an
+// error e * b^2 ~ 1e3 in its discriminant (hit points off the wall by ~0.1: self-hits in rings), so
+// the quadratic keeps a = d.d: t = k -+ sqrt(det / a), k = (op.d) / a, det = r^2 - |op - k d|^2.
 __device__ __forceinline__ float sphere_t_wide(const SPT_CONST GeoSphD& S, f3 o, f3 d) {
   const double ox = S.px - (double)o.x, oy = S.py - (double)o.y, oz = S.pz - (double)o.z;
   const double dx = d.x, dy = d.y, dz = d.z;
-  const double bb = fma(oz, dz, fma(oy, dy, ox * dx));
-  const double qx = fma(-bb, dx, ox), qy = fma(-bb, dy, oy), qz = fma(-bb, dz, oz);
+  const double a = fma(dz, dz, fma(dy, dy, dx * dx));
+  const double k = fma(oz, dz, fma(oy, dy, ox * dx)) / a;
+  const double qx = fma(-k, dx, ox), qy = fma(-k, dy, oy), qz = fma(-k, dz, oz);
   const double det = S.rad2 - fma(qz, qz, fma(qy, qy, qx * qx));
   if (!(det >= 0.0)) return 0.0f;
-  const double sd = sqrt(det);
-  const double t1 = bb - sd, t2 = bb + sd;
+  const double sd = sqrt(det / a);
+  const double t1 = k - sd, t2 = k + sd;
   return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
 }
 __device__ __forceinline__ float sphere_t_any(const SPT_CONST SceneGeo* G, int j, f3 o, f3 d) {

@@ -119,10 +119,13 @@ def variant_pins():
         json.dump(out, f, indent=1)
 
 
-def quality_c3(ref, tmp, w=1024, h=768, spp=64, seeds=range(201, 217), k=32):
+def quality_c3(ref, tmp, w=1024, h=768, spp=512, seeds=range(201, 217), k=32):
     """bench.py's `quality` fixture (`--quality-c3`): the reference's own C3 image (HEAD NEE,
-    1024x768) as 32x32-block means of its linearised PPM, one set per independent run of
-    oracle/_ref/smallpt_nee_xs at 64 spp (16 runs = 1024 spp pooled): ref_c3_blocks_k32.npz."""
+    1024x768 @ 512 spp, the bench's config) as 32x32-block means of its linearised PPM, one set
+    per independent run of oracle/_ref/smallpt_nee_xs (16 runs): ref_c3_blocks_k32.npz. The runs
+    use the bench's spp because the reference clamps each PIXEL estimate to [0, 1] (:538): the
+    clamp removes more of a noisier estimate, so images at different spp differ in expectation
+    (measured: 64-spp runs are 0.4 % darker than a 512-spp image)."""
     from concurrent.futures import ThreadPoolExecutor
 
     def run(s):
@@ -133,7 +136,7 @@ def quality_c3(ref, tmp, w=1024, h=768, spp=64, seeds=range(201, 217), k=32):
         os.remove(path)
         return lin.reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
 
-    with ThreadPoolExecutor(max(1, (os.cpu_count() or 2) - 1)) as ex:
+    with ThreadPoolExecutor(max(1, (os.cpu_count() or 2) - 2)) as ex:
         blocks = np.array(list(ex.map(run, seeds)))
     np.savez(os.path.join(HERE, f"ref_c3_blocks_k{k}.npz"), blocks=blocks, seeds=np.array(list(seeds)),
              shape=np.array([w, h, spp, k]))
