@@ -387,9 +387,11 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   if constexpr (TP::SPH) {
     const int nsph = G->n_sph, nnar = nsph - G->n_sph_wide, base = G->n_xy + G->n_xz + G->n_yz;
 #ifndef SPT_SPH_UNROLL
-#define SPT_SPH_UNROLL 8
+#define SPT_SPH_UNROLL 4
 #endif
-    // unrolled so the scalar loads of several spheres are issued before one wait
+    // unrolled so the scalar loads of several spheres are issued before one wait; 4, not 8: the
+    // 32 SGPRs of 8 spheres pushed the SGPR-capped sphere kernel to 65 VGPRs (7 waves/SIMD);
+    // at 4 it has 63 (8 waves): C5 at 256 spp 475 -> 467 ms
 #pragma unroll SPT_SPH_UNROLL
     for (int j = 0; j < nnar; ++j) {
       const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
@@ -579,8 +581,12 @@ render_kernel(const KParams* __restrict__ Pg) {
   // non-terminal vertex takes one (nee_events = vertices - samples, added by the host).
   constexpr bool kNeeByIdentity = CF::NEE == 1 && !TP::MAT;
   uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
-  uint32_t l_shadow = 0;  // shadow rays traced (NEE samples that passed light_accepts())
-  uint32_t l_sph = 0;     // vertices on a sphere (their normal is the FLOP model's sphere term)
+  // Shadow rays traced (NEE samples that passed light_accepts()): per lane in the rect kernels,
+  // wave-uniform (ballot-counted) in the sphere kernels, whose VGPR budget is the tighter one.
+  uint32_t l_shadow = 0;
+  uint32_t n_sph = 0;     // vertices on a sphere (the FLOP model's sphere-normal term): wave-uniform,
+                          // ballot-counted in the shading block (a per-lane counter cost C5's kernel
+                          // a VGPR and its 8th wave per SIMD)
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
   uint32_t reg_flags = 0;
@@ -732,7 +738,8 @@ render_kernel(const KParams* __restrict__ Pg) {
         const bool lh = id == light_id_of<CF>(D);
         if (lh) SPT_REGION(7);
         l_hit += lh ? 1u : 0u;
-        ++l_shadow;
+        if constexpr (TP::SPH) l_shadow += (uint32_t)__popcll(__ballot(true));
+        else ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
         const float pdf = fabsf(div_mk(larea * d.y, t * t));            // :471
         const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
@@ -792,7 +799,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
           if (TP::MAT) gn = n;
-          ++l_sph;
+          n_sph += (uint32_t)__popcll(__ballot(true));  // the lanes shading a sphere vertex
         }
         }
         f3 f = mk(H.cx, H.cy, H.cz);
@@ -890,8 +897,16 @@ render_kernel(const KParams* __restrict__ Pg) {
               const uint32_t ldxi = CF::LREF == 1 ? kRefLdxi : D->ldxi;
               const uint32_t ldzi = CF::LREF == 1 ? kRefLdzi : D->ldzi;
               const float lx0 = CF::LREF == 1 ? kRefLx0 : D->lx0, lz0 = CF::LREF == 1 ? kRefLz0 : D->lz0;
-              xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * ldxi), 0x1p-31f, lx0);
-              zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * ldzi), 0x1p-31f, lz0);
+              if constexpr (CF::LREF == 1) {
+                // ((r >> 8) << 7) * 36 mod 2^32 as one full-rate 24-bit multiply (the operands are
+                // 24 and 13 bits; v_mul_u32_u24 keeps the low 32 bits of the product): the same
+                // bits as the half-rate v_mul_lo_u32 and its mask
+                xl = fmaf((float)(int32_t)__umul24(r.x >> 8, kRefLdxi << 7), 0x1p-31f, lx0);
+                zl = fmaf((float)(int32_t)__umul24(r.y >> 8, kRefLdzi << 7), 0x1p-31f, lz0);
+              } else {
+                xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * ldxi), 0x1p-31f, lx0);
+                zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * ldzi), 0x1p-31f, lz0);
+              }
             } else {
               xl = fmaf(u01(r.x), D->ldx, D->lx0);
               zl = fmaf(u01(r.y), D->ldz, D->lz0);
@@ -1010,8 +1025,13 @@ render_kernel(const KParams* __restrict__ Pg) {
       atomicAdd(st + 3, (unsigned long long)l_hit);
       atomicAdd(st + 5, (unsigned long long)l_hit);
       atomicAdd(st + 7, (unsigned long long)l_miss);
-      atomicAdd(st + kStatShadowTraced, (unsigned long long)l_shadow);
-      if constexpr (TP::SPH) atomicAdd(st + kStatSphereVertices, (unsigned long long)l_sph);
+      if constexpr (TP::SPH) {
+        if (lane == 0) atomicAdd(st + kStatShadowTraced, (unsigned long long)l_shadow);
+      } else {
+        atomicAdd(st + kStatShadowTraced, (unsigned long long)l_shadow);
+      }
+      if constexpr (TP::SPH)
+        if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)n_sph);
     }
   }
 }
