@@ -528,6 +528,11 @@ render_kernel(const KParams* __restrict__ Pg) {
   // o, d, T, depth, branch.
   struct Node { float o[3], d[3], T[3]; int depth; uint32_t branch; };
   __shared__ Node s_stack[TP::MAT ? kBlock * 2 : 1];
+  // Sphere vertices shaded, per wave (SPH only). They are counted inside the divergent shading
+  // block, where a wave-uniform register would turn per-lane (a ballot there sees only the active
+  // lanes); one LDS add per wave (the atomic optimizer folds the lanes) keeps it out of the VGPRs.
+  __shared__ uint32_t s_sph[TP::SPH ? kBlock / 64 : 1];
+  if (TP::SPH && threadIdx.x < kBlock / 64) s_sph[threadIdx.x] = 0;
   {
     const SPT_CONST KParams* P = cptr(Pg);
     const SPT_CONST SceneGeo* G = cptr(P->geo);
@@ -582,11 +587,9 @@ render_kernel(const KParams* __restrict__ Pg) {
   constexpr bool kNeeByIdentity = CF::NEE == 1 && !TP::MAT;
   uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
   // Shadow rays traced (NEE samples that passed light_accepts()): per lane in the rect kernels,
-  // wave-uniform (ballot-counted) in the sphere kernels, whose VGPR budget is the tighter one.
+  // wave-uniform in the sphere kernels (a ballot of the kStShadow lanes at the convergent point
+  // before the trace), whose VGPR budget is the tighter one.
   uint32_t l_shadow = 0;
-  uint32_t n_sph = 0;     // vertices on a sphere (the FLOP model's sphere-normal term): wave-uniform,
-                          // ballot-counted in the shading block (a per-lane counter cost C5's kernel
-                          // a VGPR and its 8th wave per SIMD)
 #ifdef SPT_REGION_STATS
   uint32_t reg_exec[kRegions] = {}, reg_lanes[kRegions] = {};
   uint32_t reg_flags = 0;
@@ -714,6 +717,7 @@ render_kernel(const KParams* __restrict__ Pg) {
     // Path rays: counted here by the generic kernel only. Without SPEC/REFR every path ray is a
     // sample's camera ray or a cosine continuation, so the others add n_cos + samples at the end.
     if constexpr (TP::MAT) n_path += (uint32_t)__popcll(__ballot(ls == kStPath));
+    if constexpr (TP::SPH) l_shadow += (uint32_t)__popcll(__ballot(ls == kStShadow));
     if (ls >= kStPath) {  // kStPath or kStShadow
       // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
       SPT_REGION(4);
@@ -738,8 +742,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         const bool lh = id == light_id_of<CF>(D);
         if (lh) SPT_REGION(7);
         l_hit += lh ? 1u : 0u;
-        if constexpr (TP::SPH) l_shadow += (uint32_t)__popcll(__ballot(true));
-        else ++l_shadow;
+        if constexpr (!TP::SPH) ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
         const float pdf = fabsf(div_mk(larea * d.y, t * t));            // :471
         const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
@@ -799,7 +802,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
           if (TP::MAT) gn = n;
-          n_sph += (uint32_t)__popcll(__ballot(true));  // the lanes shading a sphere vertex
+          atomicAdd(&s_sph[threadIdx.x / 64], 1u);  // the lanes shading a sphere vertex
         }
         }
         f3 f = mk(H.cx, H.cy, H.cz);
@@ -1031,7 +1034,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         atomicAdd(st + kStatShadowTraced, (unsigned long long)l_shadow);
       }
       if constexpr (TP::SPH)
-        if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)n_sph);
+        if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)s_sph[threadIdx.x / 64]);
     }
   }
 }
