@@ -39,6 +39,15 @@ constexpr int kBlock = 256;
 // queue drains) though faster for C2 (4.45 ms); a guided scheme (static first slice per wave, then
 // shares of what is left, 16..256) was 6 % slower on C3-C5.
 constexpr uint32_t kGrab = 64;
+constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the queue atomics)
+// Launches with fewer lane-iterations per resident lane than SPT_SMALL_ITERS deal their units
+// almost all at once (SPT_SMALL_UNITS per lane) and balance by stealing (host, spt_render_async).
+#ifndef SPT_SMALL_ITERS
+#define SPT_SMALL_ITERS 2000.0
+#endif
+#ifndef SPT_SMALL_UNITS
+#define SPT_SMALL_UNITS 1.5
+#endif
 #ifdef SPT_WAVE_TIMES
 constexpr int kStatWords = 32 + 3 * 32768;  // diagnostic: per-wave start, end, iterations
 #else
@@ -112,6 +121,10 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // n / d = (n * m) >> sh for every n < 2^31 (Granlund-Montgomery, host-computed): the refill's
   // divisions by n_local_pix, width and tile_rows without the ~25-instruction integer divide.
   uint32_t m_npix, sh_npix, m_w, sh_w, m_tile, sh_tile;
+  // Guided grabs (small launches only, sh_guided < 32): a wave takes min(kGrab, max(units its
+  // lanes need, kGrabMin, left >> sh_guided)) units per queue atomic, left = units not yet handed
+  // out, so no wave hoards a full pool while the queue runs dry. sh_guided = 32: always kGrab.
+  uint32_t sh_guided;
   float inv_spp, inv_w, inv_h;
   float fix_scale;  // inv_spp * 2^31 (fix31)
   // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
@@ -480,6 +493,20 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t s
   return (uint32_t)(((uint64_t)n * m) >> sh);
 }
 
+// A local pixel index (row-tile shard order) -> the Philox pixel key and camera raster terms.
+__device__ __forceinline__ void pixel_terms(const SPT_CONST KParams* Q, uint32_t lp, PxKey& pk,
+                                            float& fx, float& fy) {
+  const uint32_t w = (uint32_t)Q->width;
+  const uint32_t lr = div_magic(lp, Q->m_w, Q->sh_w);
+  const int px = (int)(lp - lr * w);
+  const uint32_t T_ = (uint32_t)Q->tile_rows;
+  const uint32_t tile = div_magic(lr, Q->m_tile, Q->sh_tile), within = lr - tile * T_;
+  const int py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
+  pk = philox_pixel_key((uint32_t)py * w + (uint32_t)px, Q->seed);
+  fx = (float)px - 0.5f;
+  fy = (float)(Q->height - py - 1) - 0.5f;
+}
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -573,7 +600,7 @@ render_kernel(const KParams* __restrict__ Pg) {
     ck = CamK{C->cam[0], C->cam[1], C->cam[2], C->cam[3], C->cam[4], C->cam[5], C->cam[6],
               C->cam[10], C->inv_w, C->inv_h, C->fix_scale};
   }
-  uint32_t pool_next = 0, pool_end = 0;
+  uint32_t pool_next = 0, pool_end = 0, grab_at = 0;  // grab_at: the wave's last queue position
   bool exhausted = false, capped = false;
   // Wave-uniform event counters (SGPRs), fed by ballots at convergent points of the loop: per-lane
   // counters incremented inside the divergent blocks cost ~40 VGPRs of copies.
@@ -634,12 +661,18 @@ render_kernel(const KParams* __restrict__ Pg) {
       SPT_REGION(2);
       const SPT_CONST KParams* Q = cptr(Pg);
       if (pool_next >= pool_end) {
+        uint32_t want = kGrab;
+        if (Q->sh_guided < 32u) {
+          const uint32_t left = Q->n_units - min(grab_at, (uint32_t)Q->n_units);
+          want = min(kGrab, max(max((uint32_t)__popcll(need), kGrabMin), left >> Q->sh_guided));
+        }
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(Q->queue, kGrab);
+        if (lane == 0) b = atomicAdd(Q->queue, want);
         b = __builtin_amdgcn_readfirstlane(b);
+        grab_at = b + want;
         if (b >= Q->n_units) { exhausted = true; break; }
         pool_next = b;
-        pool_end = min(b + kGrab, Q->n_units);
+        pool_end = min(b + want, Q->n_units);
       }
       const uint32_t rank = lane_rank(need);
       const uint32_t avail = pool_end - pool_next;
@@ -650,20 +683,49 @@ render_kernel(const KParams* __restrict__ Pg) {
         lp = u - j * npix;
         s = j * (uint32_t)Q->chunk;
         s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
-        const uint32_t lr = div_magic(lp, Q->m_w, Q->sh_w);
-        const int px = (int)(lp - lr * w);
-        const uint32_t T_ = (uint32_t)Q->tile_rows;
-        const uint32_t tile = div_magic(lr, Q->m_tile, Q->sh_tile), within = lr - tile * T_;
-        const int py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
-        pk = philox_pixel_key((uint32_t)py * w + (uint32_t)px, Q->seed);
-        fx = (float)px - 0.5f;
-        fy = (float)(Q->height - py - 1) - 0.5f;
+        (void)w;
+        pixel_terms(Q, lp, pk, fx, fy);
         ls = kStCam;
         needs_unit = false;
       }
       pool_next += min((uint32_t)__popcll(need), avail);
       need = __ballot(needs_unit);
     }
+#ifndef SPT_NO_STEAL
+    // 2b) the queue is dry: an idle lane takes the upper half of a busy lane's unstarted samples
+    //     (same pixel; each flushes its own sums and the accumulation is integer, so the image is
+    //     unchanged). A wave's tail is then ~one path instead of ~one unit. Pairs are made by a
+    //     scalar loop over the lane masks (readlane + a per-lane select), only in the tail.
+    if (exhausted) {
+      uint64_t idle = __ballot(ls == kStIdle);
+      if (idle != 0) {
+        const uint32_t cur = s + (ls == kStCam ? 0u : 1u);  // first unstarted sample
+        uint64_t dm = __ballot(ls != kStIdle && s_end > cur + (ls == kStCam ? 1u : 0u));
+        while (idle != 0 && dm != 0) {
+          const int il = __builtin_ctzll(idle), dl = __builtin_ctzll(dm);
+          idle &= idle - 1;
+          dm &= dm - 1;
+          const uint32_t dcur = (uint32_t)__builtin_amdgcn_readlane((int)cur, dl);
+          const uint32_t dend = (uint32_t)__builtin_amdgcn_readlane((int)s_end, dl);
+          const uint32_t mid = dcur + (dend - dcur) / 2u;  // donor keeps [.., mid), taker [mid, dend)
+          const uint32_t d_lp = (uint32_t)__builtin_amdgcn_readlane((int)lp, dl);
+          const uint32_t d_hi = (uint32_t)__builtin_amdgcn_readlane((int)pk.hi, dl);
+          const uint32_t d_lo = (uint32_t)__builtin_amdgcn_readlane((int)pk.lo, dl);
+          const float d_fx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fx), dl));
+          const float d_fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy), dl));
+          const bool tk = lane == (uint32_t)il;  // the taker
+          s_end = tk ? dend : (lane == (uint32_t)dl ? mid : s_end);
+          s = tk ? mid : s;
+          lp = tk ? d_lp : lp;
+          pk.hi = tk ? d_hi : pk.hi;
+          pk.lo = tk ? d_lo : pk.lo;
+          fx = tk ? d_fx : fx;
+          fy = tk ? d_fy : fy;
+          ls = tk ? kStCam : ls;
+        }
+      }
+    }
+#endif
     if (__ballot(ls != kStIdle) == 0) break;
     n_cos += (uint32_t)__popcll(__ballot(ls == kStCos));
 
@@ -1431,17 +1493,33 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // 25.0 ms vs 26.0 ms at 8 units/lane and 27.8 ms at 2); never changes results (integer
   // accumulation).
   int chunk = p->chunk;
+  const double lanes = (double)c->n_cu * c->bpc[kv] * kBlock;  // resident lanes of THIS kernel
+  const double rays_per_sample = p->nee_prob > 0.0f ? 5.3 : 8.9;  // HEAD: NEE / cosine only
+  const double lane_iters = (double)K.n_local_pix * p->spp * rays_per_sample / lanes;
+  const bool small_launch = lane_iters < SPT_SMALL_ITERS;
   if (chunk <= 0) {
-    const double lanes = (double)c->n_cu * c->bpc[kv] * kBlock;  // resident lanes of THIS kernel
-    const double want_units = 16.0 * lanes;
-    const double per_pix = std::max(1.0, want_units / std::max(1, K.n_local_pix));
-    chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
+    if (small_launch) {
+      // A short launch (C2: ~860 lane-iterations per lane): deal ~SPT_SMALL_UNITS units per lane
+      // and let the in-wave stealing and guided grabs balance the rest (C2: chunk 23 -> 64,
+      // 4.6 -> 4.0 ms; measured, tools/ab_r02*.sh).
+      const double units_per_pix = std::max(1.0, std::ceil(SPT_SMALL_UNITS * lanes / std::max(1, K.n_local_pix)));
+      chunk = (int)std::ceil(p->spp / units_per_pix);
+    } else {
+      // ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured 25.0 ms
+      // vs 26.0 ms at 8 units/lane and 27.8 ms at 2)...
+      const double per_pix = std::max(1.0, 16.0 * lanes / std::max(1, K.n_local_pix));
+      chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
+    }
     // ...but a unit should last >= ~200 lane-iterations: every unit costs a refill (~35 VALU +
-    // ~40 SALU for the whole wave) and a retire. Rays per sample at HEAD: 5.3 with NEE, 8.9
-    // cosine-only (C2: 6 -> 23 samples per unit, 4.73 -> ~4.6 ms; C3 stays at 48).
-    const double rays_per_sample = p->nee_prob > 0.0f ? 5.3 : 8.9;
+    // ~40 SALU for the whole wave) and a retire (C2: 6 -> 23 samples per unit, 4.73 -> ~4.6 ms).
     chunk = std::max(chunk, (int)std::ceil(200.0 / rays_per_sample));
     chunk = std::min(chunk, p->spp);
+  }
+  {
+    const uint32_t waves = (uint32_t)(c->n_cu * c->bpc[kv] * (kBlock / 64));
+    uint32_t sh = 1;  // 2^sh >= 2 x waves
+    while ((1u << sh) < 2u * waves && sh < 31) ++sh;
+    K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
   }
   K.chunk = chunk;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
