@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import importlib
+import glob
 import json
 import os
 import sys
@@ -232,6 +233,8 @@ def main() -> None:
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
                     help="PMC traffic summary (HBM bytes per render launch) to attach, if present")
     ap.add_argument("--save-ppm", default="")
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="rank 0 re-renders the whole image alone and checks the gathered one bit for bit")
     args = ap.parse_args()
 
     import torch
@@ -337,18 +340,27 @@ def main() -> None:
         except Exception:  # noqa: BLE001
             traffic = None
     pmc = {}
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-    if os.path.exists(pmc_path) and args.config == "c3" and world == 1:
+    # the newest round's PMC summary (scripts/update_profiles.py)
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_summary.json")))
+    pmc_path = pmcs[-1] if pmcs else ""
+    if pmc_path and args.config == "c3" and world == 1:
         try:
             der = json.load(open(pmc_path))["derived"]
             pmc = {"valu_issue_frac": round(der["valu_issue_frac_of_peak"], 3),
                    "valu_lane_utilization": round(der["valu_lane_utilization"], 3),
-                   "source": "profiles/r01_pmc_summary.json (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU)"}
+                   "source": f"profiles/{os.path.basename(pmc_path)} (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU)"}
         except Exception:  # noqa: BLE001
             pmc = {}
 
+    gather_exact = None
     if rank == 0:
         img = full.cpu().numpy()
+        if args.verify_gather:  # the whole image on this GPU alone (1 shard) must equal the gather
+            p1 = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
+                                    max_depth=cfg["max_depth"], tile_rows=8, device=local)
+            one = spt.render(prims, cam, p1)
+            gather_exact = bool(np.array_equal(one, img))
+            assert gather_exact, "gathered image differs from the 1-GPU render"
         cpu = None
         port = None
         if not args.no_cpu_baseline and world == 1:
@@ -408,6 +420,7 @@ def main() -> None:
                                                       / my_samples, 4),
                       "misses_per_sample": round(s0["misses"] / my_samples, 4)},
             "quality": qual,
+            "gather_equals_1gpu_render": gather_exact,
             "cpu_baseline": cpu,
             "image_writer": writer,
         }
