@@ -233,6 +233,8 @@ def main() -> None:
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
                     help="PMC traffic summary (HBM bytes per render launch) to attach, if present")
     ap.add_argument("--save-ppm", default="")
+    ap.add_argument("--kernel-level", default="auto", help="A/B only: cap the kernel specialisation "
+                    "(auto | generic | cornell | const; spt_params.flags, never changes results)")
     ap.add_argument("--verify-gather", action="store_true",
                     help="rank 0 re-renders the whole image alone and checks the gathered one bit for bit")
     args = ap.parse_args()
@@ -268,7 +270,8 @@ def main() -> None:
     cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
     params = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
                                 max_depth=cfg["max_depth"], tile_rows=8, shard_index=rank,
-                                shard_count=world, device=local, chunk=args.chunk)
+                                shard_count=world, device=local, chunk=args.chunk,
+                                flags=spt.kernel_flag(args.kernel_level))
     rows_of = sd.shard_row_lists(h, 8, world)
     my_rows = rows_of[rank]
     assert np.array_equal(spt.shard_rows(params), my_rows)

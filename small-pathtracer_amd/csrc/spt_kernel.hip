@@ -305,6 +305,9 @@ __device__ __forceinline__ int pair_pos(CornellTestPtr<J>, uint64_t sel1) {
 __device__ __forceinline__ int pair_pos(const SPT_CONST GeoTest* g, uint64_t sel1) {
   return sel_i(sel1, g->pos0, g->pos1);
 }
+__device__ __forceinline__ int pair_pos(const GeoTest* g, uint64_t sel1) {  // LDS copy (A/B)
+  return sel_i(sel1, g->pos0, g->pos1);
+}
 template <int J>
 __device__ __forceinline__ void cornell_test(const Ray6* rays, const uint64_t* up, uint32_t& tmin_key,
                                              int& pos) {
@@ -318,9 +321,9 @@ __device__ __forceinline__ void cornell_tests(std::integer_sequence<int, J...>, 
   (cornell_test<J>(rays, up, tmin_key, pos), ...);
 }
 
-template <int N>  // the tests of one kind group, uploaded geometry (every test as a pair)
-__device__ __forceinline__ void test_group(const SPT_CONST GeoTest* g, int n_rt, const Ray6& r,
-                                           uint32_t& tmin_key, int& pos) {
+template <int N, class GT>  // the tests of one kind group, uploaded geometry (every test as a pair)
+__device__ __forceinline__ void test_group(GT g, int n_rt, const Ray6& r, uint32_t& tmin_key,
+                                           int& pos) {
   const uint64_t up = lanes(r.ia > 0.0f);
   if constexpr (N >= 0) {
 #pragma unroll
@@ -339,7 +342,9 @@ __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   return RectHit{tt, (bool)((int)ia & (int)ib)};
 }
 
-__device__ __forceinline__ float sphere_t(const SPT_CONST GeoSph& S, f3 o, f3 d) {
+struct alignas(16) SphLds { float px, py, pz, rad2; };  // a narrow sphere's LDS copy
+template <class SP>
+__device__ __forceinline__ float sphere_t(const SP& S, f3 o, f3 d) {
   // det = r^2 - |op - b d|^2; nearest root beyond the fp32 epsilon (Sphere::intersect :229-239)
   const f3 op = mk(S.px - o.x, S.py - o.y, S.pz - o.z);
   const float bb = dot3(op, d);
@@ -377,10 +382,41 @@ __device__ __forceinline__ float sphere_t_any(const SPT_CONST SceneGeo* G, int j
 template <class TP>
 __device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; }
 
-template <class TP, class GP>
-__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect,
-                                                const int* pos2idx, f3 o, f3 d, float& t_out,
-                                                int& id, float& ia_hit) {
+// The uploaded scene's rect tests are read from an LDS copy staged once per block (ds_read
+// broadcasts into VGPRs) -- the north star's "geometry staged once into LDS". A/B (DESIGN.md
+// section 4, scripts/ab_r02g.sh): faster than scalar loads through the constant address space
+// (-DSPT_GEO_SLOAD): generic kernel at C3 27.65 -> 26.26 ms, HEAD-topology kernel 19.1 -> 18.5 ms,
+// C5 at 256 spp 460 -> 453.6 ms. Spheres stay on scalar loads (an LDS copy, -DSPT_SPH_LDS, cost
+// C5 1.4 %: four VGPRs per unrolled sphere). The HEAD scene itself runs with its bounds as
+// instruction literals (15.5 ms).
+// (the fp64 wide-sphere kernel keeps scalar loads: its VGPR budget is the tight one, 78 vs 90)
+template <class TP>
+__device__ __forceinline__ auto tests_of(const SPT_CONST SceneGeo* G, const GeoTest* lds) {
+#ifdef SPT_GEO_SLOAD
+  constexpr bool kLds = false;
+#else
+  constexpr bool kLds = !TP::WIDE;
+#endif
+  if constexpr (TP::CONSTGEO) {
+    (void)G; (void)lds;
+    return (const SPT_CONST GeoTest*)nullptr;  // the HEAD tests are literals (kCornellTests)
+  } else if constexpr (kLds) {
+    (void)G;
+    return lds;
+  } else {
+    (void)lds;
+    return G->test + 0;
+  }
+}
+#ifdef SPT_SPH_LDS
+#define SPT_SPHS(G) s_sph
+#else
+#define SPT_SPHS(G) (G)->sph
+#endif
+template <class TP, class GP, class GT, class SP>
+__device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect, GT tests,
+                                                SP sphs, const int* pos2idx, f3 o, f3 d,
+                                                float& t_out, int& id, float& ia_hit) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
   uint32_t tmin_key = tkey(1e20f);
   int pos = -1;
@@ -392,9 +428,9 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   } else {
     const int ntxy = n_of<TP>(TP::NTXY, G->n_txy), ntxz = n_of<TP>(TP::NTXZ, G->n_txz);
     const int ntyz = n_of<TP>(TP::NTYZ, G->n_tyz);
-    test_group<TP::NTXY>(G->test, ntxy, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
-    test_group<TP::NTXZ>(G->test + ntxy, ntxz, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
-    test_group<TP::NTYZ>(G->test + ntxy + ntxz, ntyz, ray6<0>(o, d, ix, iy, iz), tmin_key, pos);
+    test_group<TP::NTXY>(tests, ntxy, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
+    test_group<TP::NTXZ>(tests + ntxy, ntxz, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
+    test_group<TP::NTYZ>(tests + ntxy + ntxz, ntyz, ray6<0>(o, d, ix, iy, iz), tmin_key, pos);
   }
   (void)rect;
   if constexpr (TP::SPH) {
@@ -407,7 +443,7 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     // at 4 it has 63 (8 waves): C5 at 256 spp 475 -> 467 ms
 #pragma unroll SPT_SPH_UNROLL
     for (int j = 0; j < nnar; ++j) {
-      const uint32_t kk = tkey(sphere_t(G->sph[j], o, d));
+      const uint32_t kk = tkey(sphere_t(sphs[j], o, d));
       const bool acc = kk < tmin_key;
       tmin_key = acc ? kk : tmin_key;
       pos = acc ? base + j : pos;
@@ -551,6 +587,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(SPT_NUM
 render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
+  __shared__ GeoTest s_test[TP::CONSTGEO || TP::WIDE ? 1 : kMaxPrims];
+#ifdef SPT_SPH_LDS
+  __shared__ SphLds s_sph[TP::SPH ? kMaxPrims : 1];
+#endif
   // Pending REFR refraction children (:494-495 at depth <= 2), two per lane at most (MAT only):
   // o, d, T, depth, branch.
   struct Node { float o[3], d[3], T[3]; int depth; uint32_t branch; };
@@ -558,8 +598,8 @@ render_kernel(const KParams* __restrict__ Pg) {
   // Sphere vertices shaded, per wave (SPH only). They are counted inside the divergent shading
   // block, where a wave-uniform register would turn per-lane (a ballot there sees only the active
   // lanes); one LDS add per wave (the atomic optimizer folds the lanes) keeps it out of the VGPRs.
-  __shared__ uint32_t s_sph[TP::SPH ? kBlock / 64 : 1];
-  if (TP::SPH && threadIdx.x < kBlock / 64) s_sph[threadIdx.x] = 0;
+  __shared__ uint32_t s_nsph[TP::SPH ? kBlock / 64 : 1];
+  if (TP::SPH && threadIdx.x < kBlock / 64) s_nsph[threadIdx.x] = 0;
   {
     const SPT_CONST KParams* P = cptr(Pg);
     const SPT_CONST SceneGeo* G = cptr(P->geo);
@@ -567,6 +607,16 @@ render_kernel(const KParams* __restrict__ Pg) {
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
       s_prims[i] = P->prims[i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
+      if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz) {
+        const SPT_CONST GeoTest& q = G->test[i];
+        s_test[i] = GeoTest{q.k0, q.k1, q.ma, q.ha, q.mb, q.hb, q.pos0, q.pos1};
+      }
+#ifdef SPT_SPH_LDS
+      if (TP::SPH && i < G->n_sph) {
+        const SPT_CONST GeoSph& q = G->sph[i];
+        s_sph[i] = SphLds{q.px, q.py, q.pz, q.rad2};
+      }
+#endif
     }
   }
   __syncthreads();
@@ -786,11 +836,11 @@ render_kernel(const KParams* __restrict__ Pg) {
       const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
       int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
       float t, ia_hit;
-      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, o, d, t, id, ia_hit);
+      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), SPT_SPHS(G), s_pos2idx, o, d, t, id, ia_hit);
       if (SPT_PROBE & 2) {
         float t2, ia2;
         int id2 = id;
-        const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2, ia2);
+        const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), SPT_SPHS(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2, ia2);
         if (opq(0u) != 0u) { hit = h2; t = t2; id = id2; ia_hit = ia2; }
       }
 
@@ -864,7 +914,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
           if (TP::MAT) gn = n;
-          atomicAdd(&s_sph[threadIdx.x / 64], 1u);  // the lanes shading a sphere vertex
+          atomicAdd(&s_nsph[threadIdx.x / 64], 1u);  // the lanes shading a sphere vertex
         }
         }
         f3 f = mk(H.cx, H.cy, H.cz);
@@ -1096,7 +1146,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         atomicAdd(st + kStatShadowTraced, (unsigned long long)l_shadow);
       }
       if constexpr (TP::SPH)
-        if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)s_sph[threadIdx.x / 64]);
+        if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)s_nsph[threadIdx.x / 64]);
     }
   }
 }
