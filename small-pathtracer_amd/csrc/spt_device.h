@@ -85,11 +85,12 @@ __device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
 }
 
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
-// 16-bit draw from the low bytes of two Philox words (RR and NEE-mix draws, see the kernel).
-__device__ __forceinline__ float u16(uint32_t lo, uint32_t hi) {
-  // (lo & 0xFF) | (hi & 0xFF) << 8 as ONE v_perm_b32 (bytes {hi:lo}[4], [0], zero, zero)
-  return (float)__builtin_amdgcn_perm(hi, lo, 0x0C0C0400u) * 0x1p-16f;
+// 16-bit draw from the low bytes of two Philox words (RR and NEE-mix draws, camera jitter; see
+// the kernel): (lo & 0xFF) | (hi & 0xFF) << 8 as ONE v_perm_b32 (bytes {hi:lo}[4], [0], 0, 0).
+__device__ __forceinline__ uint32_t u16i(uint32_t lo, uint32_t hi) {
+  return __builtin_amdgcn_perm(hi, lo, 0x0C0C0400u);
 }
+__device__ __forceinline__ float u16(uint32_t lo, uint32_t hi) { return (float)u16i(lo, hi) * 0x1p-16f; }
 
 // ---- deterministic reciprocal / reciprocal square root (contract): integer seed + 3 Newton
 // steps; max relative error 6e-8 / 1.3e-7 (oracle tests). rcp_nr(+-0) is NaN, which the

@@ -76,7 +76,11 @@ struct alignas(16) DevPrim {
   int refl;  // spt_refl
   float ip;  // 1/pmax, correctly rounded on the host (the RR reweighting f * (1/p) of :451)
   float ex, ey, ez, pmax;
-  float cx, cy, cz, pad2;
+  float cx, cy, cz;
+  // Russian roulette as integers (host): INT_MIN when pmax == 0 (RR always applies, :448), else
+  // ceil(pmax * 2^16) (0 for pmax <= 0, 2^16 for pmax >= 1), so that `u16 * 2^-16 < pmax` (:449,
+  // with alive only for pmax > 0) is `(int)u16 < rr_t`: the same decision with no conversion
+  int32_t rr_t;
 };
 static_assert(sizeof(DevPrim) == 64, "DevPrim layout");
 
@@ -804,12 +808,13 @@ render_kernel(const KParams* __restrict__ Pg) {
         const SPT_CONST KParams* C = cptr(Pg);
         f3 vc;
         if constexpr (CF::CAMAX == 1) {  // fma(+-0, s, a) == a for a != 0; a == +-0 only meets - o
-          const float su = (fx + u16(r.x, r.y)) * ck.iw;
-          const float sv = (fy + u16(r.z, r.w)) * ck.ih;
+          // fx + u * 2^-16 in one fma (the product is exact: the same single rounding as the add)
+          const float su = fmaf((float)u16i(r.x, r.y), 0x1p-16f, fx) * ck.iw;
+          const float sv = fmaf((float)u16i(r.z, r.w), 0x1p-16f, fy) * ck.ih;
           vc = mk(fmaf(ck.h0, su, ck.l0) - ck.o0, fmaf(ck.v1, sv, ck.l1) - ck.o1, ck.l2 - ck.o2);
         } else {
-          const float su = (fx + u16(r.x, r.y)) * C->inv_w;
-          const float sv = (fy + u16(r.z, r.w)) * C->inv_h;
+          const float su = fmaf((float)u16i(r.x, r.y), 0x1p-16f, fx) * C->inv_w;
+          const float sv = fmaf((float)u16i(r.z, r.w), 0x1p-16f, fy) * C->inv_h;
           vc = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
                   fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
                   fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
@@ -919,7 +924,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         }
         f3 f = mk(H.cx, H.cy, H.cz);
         const f3 e = mk(H.ex, H.ey, H.ez);
-        const float p = H.pmax;
+        const int rr_t = H.rr_t;
         ++depth;
         u4 rl = r;  // RR / NEE-mix draws; at vertex 1 from stream 1 (only configs that need them)
         if (CF::NOS1 != 1 && depth == 1) {
@@ -932,8 +937,8 @@ render_kernel(const KParams* __restrict__ Pg) {
         // ends here.
         const int max_depth = CF::MAXD0 == 1 ? 0 : P->max_depth;
         const bool capd = (max_depth > 0) & (depth >= max_depth);
-        const bool rr = (depth > rr_depth_of<CF>(P)) | (p == 0.0f);
-        const bool alive = (p > 0.0f) & ((!(p < 1.0f)) | (u16(rl.x, rl.y) < p));
+        const bool rr = (depth > rr_depth_of<CF>(P)) | (rr_t < 0);   // p == 0
+        const bool alive = (int)u16i(rl.x, rl.y) < rr_t;              // (p > 0) & (p >= 1 | u16 < p)
         const bool term = capd | (rr & !alive);
         const float ip = keep(H.ip);  // == 1.0f / p, read unconditionally (no branch)
         const float fsc = rr ? ip : 1.0f;
@@ -1275,6 +1280,12 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
     P.cx = (float)s[i].c[0]; P.cy = (float)s[i].c[1]; P.cz = (float)s[i].c[2];
     P.pmax = P.cx > P.cy && P.cx > P.cz ? P.cx : P.cy > P.cz ? P.cy : P.cz;  // :447
     P.ip = 1.0f / P.pmax;  // IEEE single division, as the device's 1.0f / p
+    // u * 2^-16 < p (u < 2^16 an integer, p * 2^16 exact) <=> u < ceil(p * 2^16): the RR draw as
+    // one integer compare instead of a conversion, a scale and a float compare (same decision)
+    P.rr_t = P.pmax == 0.0f ? INT32_MIN
+             : !(P.pmax > 0.0f) ? 0
+             : P.pmax >= 1.0f   ? 65536
+                                : (int32_t)std::ceil((double)P.pmax * 65536.0);
     P.refl = s[i].refl;
     out[i] = P;
   }
