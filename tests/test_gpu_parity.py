@@ -173,6 +173,18 @@ def test_high_spp_tiny_image(spt, oracle):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+@pytest.mark.parametrize("w,h,spp,est", [(2, 2, 4096, 1.0), (3, 1, 2048, 0.0), (1, 1, 999, 1.0)])
+def test_in_wave_stealing_bit_exact(spt, oracle, w, h, spp, est):
+    """One unit per pixel (chunk = spp): a handful of units for a whole GPU, so the queue is dry
+    at once and the samples are spread over lanes only by the in-wave stealing (an idle lane takes
+    the upper half of a busy lane's unstarted samples). Each part flushes its own fixed-point sums:
+    the image and the path statistics stay exactly the oracle's."""
+    p = spt.default_params(width=w, height=h, spp=spp, seed=5, nee_prob=est, chunk=spp)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
 def test_chunk_size_never_changes_results(spt):
     cam = spt.Camera(aspect=40 / 30)
     imgs = [spt.render(spt.cornell_scene(), cam, spt.default_params(width=40, height=30, spp=24, chunk=c))
