@@ -547,6 +547,7 @@ typedef struct {
   float k;                 /* rect: plane coordinate */
   float ma, ha, mb, hb;    /* rect: in-plane bounds as |a - ma| <= ha, |b - mb| <= hb */
   float rad2, px, py, pz;  /* sphere */
+  float inv_r;             /* sphere: 1/r (float division), the normal is (x - p) * inv_r */
   double drad2, dpx, dpy, dpz; /* sphere in fp64 (wide: radius >= SPT_WIDE_SPHERE_RADIUS) */
   int wide;
   fv e, c;
@@ -879,7 +880,9 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
       case SPT_RECT_YZ: nl = d.x < 0.0f ? fv3(1, 0, 0) : fv3(-1, 0, 0); gn = fv3(1, 0, 0); break;
       default: {
         st->sphere_vertices++;
-        gn = fnormalize(fv3(x.x - H->px, x.y - H->py, x.z - H->pz));
+        /* Sphere::normal :248, (x - p).norm(), as (x - p) * (1/r): the hit point lies on the
+         * sphere to ~1e-7, so this is the unit normal without a reciprocal square root */
+        gn = fv3((x.x - H->px) * H->inv_r, (x.y - H->py) * H->inv_r, (x.z - H->pz) * H->inv_r);
         nl = fdot(gn, d) < 0.0f ? gn : fv3(-gn.x, -gn.y, -gn.z);
       }
     }
@@ -1050,6 +1053,7 @@ static void c_prims_from_spt(const spt_prim* s, int n, c_prim* out) {
     if (s[i].kind == SPT_SPHERE) {
       P->rad2 = (float)s[i].geom[0] * (float)s[i].geom[0];
       P->px = (float)s[i].geom[1]; P->py = (float)s[i].geom[2]; P->pz = (float)s[i].geom[3];
+      P->inv_r = 1.0f / (float)s[i].geom[0];
       P->wide = s[i].geom[0] >= SPT_WIDE_SPHERE_RADIUS;
       P->drad2 = s[i].geom[0] * s[i].geom[0];
       P->dpx = s[i].geom[1]; P->dpy = s[i].geom[2]; P->dpz = s[i].geom[3];

@@ -69,7 +69,7 @@ constexpr uint32_t kMaxWaveIters = 1u << 26;
 [[maybe_unused]] constexpr int kStatShadowTraced = 8, kStatSphereVertices = 9, kStatRegion = 12;
 
 // 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
-// axes in (x,y,z) order); sphere: w1..w4 = px, py, pz, rad^2.
+// axes in (x,y,z) order); sphere: w1..w5 = px, py, pz, rad^2, 1/rad.
 struct alignas(16) DevPrim {
   int kind;
   float w1, w2, w3, w4, w5;
@@ -918,7 +918,9 @@ render_kernel(const KParams* __restrict__ Pg) {
           nl = d.x < 0.0f ? mk(1, 0, 0) : mk(-1, 0, 0);
           if (TP::MAT) gn = mk(1, 0, 0);
         } else {
-          const f3 n = normalize3(mk(x.x - H.w1, x.y - H.w2, x.z - H.w3));
+          // Sphere::normal :248 as (x - p) * (1/r): x lies on the sphere to ~1e-7, so this is the
+          // unit normal without the normalize's rsq (contract, oracle c_path; C5 -0.7 %)
+          const f3 n = mk((x.x - H.w1) * H.w5, (x.y - H.w2) * H.w5, (x.z - H.w3) * H.w5);
           nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
           if (TP::MAT) gn = n;
           atomicAdd(&s_nsph[threadIdx.x / 64], 1u);  // the lanes shading a sphere vertex
@@ -1273,6 +1275,7 @@ static void to_dev(const spt_prim* s, int n, DevPrim* out) {
       const float r = (float)s[i].geom[0];
       P.w1 = (float)s[i].geom[1]; P.w2 = (float)s[i].geom[2]; P.w3 = (float)s[i].geom[3];
       P.w4 = r * r;
+      P.w5 = 1.0f / r;  // the normal as (x - p) * (1/r) (contract, oracle c_path)
     } else {
       P.w1 = plane_k(s[i].geom[4]);  // contract plane coordinate (spt_cornell.h)
       P.w2 = (float)s[i].geom[0]; P.w3 = (float)s[i].geom[1];
