@@ -653,16 +653,15 @@ static float c_sphere_wide(const c_prim* P, fv o, fv d) {
   return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
 }
 
-/* A narrow sphere in fp32: det = r^2 - |op - b d|^2 (cancellation-free form of :233), the nearest
- * root beyond the fp32 epsilon 2e-3; 0 = no hit. The root of det is det * rsq_nr(det) (the
+/* A narrow sphere in fp32: det = b^2 - op.op + r^2 (:233, as one fma), the nearest root beyond
+ * the fp32 epsilon 2e-3; 0 = no hit. The root of det is det * rsq_nr(det) (the
  * contract's reciprocal square root, ~1e-7 relative; det = 0 gives 0), not an IEEE sqrtf: on the
  * GPU the correctly rounded square root is an ~18-slot sequence (C5: -5.6 %). Pinned against the
  * reference's own fp64 Sphere by the sph/sph16 P2 runs. */
 static float c_sphere(const c_prim* P, fv o, fv d) {
   const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
   const float bb = fdot(op, d);
-  const fv q = fv3(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-  const float det = P->rad2 - fdot(q, q);
+  const float det = fmaf(bb, bb, P->rad2 - fdot(op, op)); /* :233's b*b - op.op + rad*rad */
   float sd, t1, t2;
   if (!(det >= 0.0f)) return 0.0f;
   sd = det * spt_oracle_rsq_nr(det);

@@ -349,11 +349,12 @@ __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
 struct alignas(16) SphLds { float px, py, pz, rad2; };  // a narrow sphere's LDS copy
 template <class SP>
 __device__ __forceinline__ float sphere_t(const SP& S, f3 o, f3 d) {
-  // det = r^2 - |op - b d|^2; nearest root beyond the fp32 epsilon (Sphere::intersect :229-239)
+  // Sphere::intersect :229-239 in the reference's own form det = b^2 - op.op + r^2 (:233), as
+  // fma(b, b, r^2 - op.op); nearest root beyond the fp32 epsilon. (Round 2: the cancellation-free
+  // r^2 - |op - b d|^2 cost 2 more VALU per sphere: C5 at 256 spp 430.4 -> 406.5 ms.)
   const f3 op = mk(S.px - o.x, S.py - o.y, S.pz - o.z);
   const float bb = dot3(op, d);
-  const f3 q = mk(fmaf(-bb, d.x, op.x), fmaf(-bb, d.y, op.y), fmaf(-bb, d.z, op.z));
-  const float det = S.rad2 - dot3(q, q);
+  const float det = fmaf(bb, bb, S.rad2 - dot3(op, op));
   if (!(det >= 0.0f)) return 0.0f;
   // the root as det * rsq_nr(det) (contract, oracle c_sphere): the IEEE sqrtf sequence costs ~18
   // issue slots, this 13 (C5 at 256 spp 452.8 -> 427.3 ms); det = 0 gives 0
