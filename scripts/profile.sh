@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}; shift || true
-ARGS=${*:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${*:---steps 6 --warmup 2 --no-cpu-baseline}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 run() {  # name, rocprof args...
