@@ -7,14 +7,15 @@
 //     loop in registers (T = throughput, L = radiance so far);
 //   * work units = (pixel, chunk of samples); a wave pulls units from a global atomic queue and
 //     hands them to its idle lanes with a ballot + mbcnt prefix sum, so lanes whose paths end by
-//     Russian roulette / light hits immediately start the next sample (no idle SIMD slots until
-//     the queue drains);
-//   * the scene (<= 64 primitives) is read with wave-uniform scalar loads in the intersect loop
-//     (intersect() :323-335 is a broadcast, never a per-lane HBM read) and staged into LDS for
-//     the per-lane (divergent) lookups of the hit primitive;
+//     Russian roulette / light hits immediately start the next sample; once the queue is dry an
+//     idle lane takes the upper half of a busy lane's unstarted samples (in-wave stealing);
+//   * the scene (<= 64 primitives) never costs a per-lane HBM read in intersect() :323-335: the
+//     reference's HEAD scene is compiled into the instruction stream, other scenes' rect tests are
+//     staged once per block into LDS (broadcast reads) and their spheres read with wave-uniform
+//     scalar loads; the per-lane lookups of the hit primitive (material) come from LDS;
 //   * Philox4x32-10 counter RNG keyed by (seed; pixel, sample, vertex, stream);
-//   * per-pixel accumulation in 32.32 fixed point with 64-bit integer atomics: exact, independent
-//     of unit size, lane order, queue order and GPU count.
+//   * per-pixel accumulation in 1.31 fixed point with 64-bit integer atomics: exact, independent
+//     of unit size, lane order, queue order, stealing and GPU count.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
