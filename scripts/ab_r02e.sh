@@ -1,5 +1,7 @@
 #!/usr/bin/env bash
 # A/B: in-wave stealing + small-launch unit policy; then the GPU parity suite.
+# Build first (CPU): scripts/build_variants.sh cur:"" nosteal:"-DSPT_NO_STEAL" \
+#   su1:"-DSPT_SMALL_UNITS=1.0" su2:"-DSPT_SMALL_UNITS=2.0" su3:"-DSPT_SMALL_UNITS=3.0"
 set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp

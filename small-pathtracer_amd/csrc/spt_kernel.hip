@@ -1569,7 +1569,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     if (small_launch) {
       // A short launch (C2: ~860 lane-iterations per lane): deal ~SPT_SMALL_UNITS units per lane
       // and let the in-wave stealing and guided grabs balance the rest (C2: chunk 23 -> 64,
-      // 4.6 -> 4.0 ms; measured, tools/ab_r02*.sh).
+      // 4.6 -> 4.0 ms; measured, scripts/ab_r02e.sh).
       const double units_per_pix = std::max(1.0, std::ceil(SPT_SMALL_UNITS * lanes / std::max(1, K.n_local_pix)));
       chunk = (int)std::ceil(p->spp / units_per_pix);
     } else {
