@@ -476,12 +476,12 @@ float spt_oracle_rsq_nr(float x) {
   }
   return y;
 }
-/* Vec::norm :50-52 as v * rsq(len2); exactly-unit vectors are returned unchanged. */
+/* Vec::norm :50-52 as v * rsq_nr(len2). (Round 1 returned exactly-unit vectors unchanged, as the
+ * reference's fp64 1/sqrt(1) does; rsq_nr(1) is 1 - 2^-24, and the select cost every normalize two
+ * VALU on the GPU for vectors that occur with probability ~2^-24.) */
 static inline fv fnormalize(fv v) {
   const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
-  float inv;
-  if (l2 == 1.0f) return v;
-  inv = spt_oracle_rsq_nr(l2);
+  const float inv = spt_oracle_rsq_nr(l2);
   return fv3(v.x * inv, v.y * inv, v.z * inv);
 }
 static inline fv fcross(fv a, fv b) {
@@ -804,12 +804,10 @@ static float c_hit_t(float n, float da, float t) {
   return fmaf(fmaf(-t, da, n), spt_oracle_rcp_nr(da), t);
 }
 /* n / d in the contract where the reference divides once per event (the NEE pdf :471):
- * q = n * rcp_nr(d) and one Markstein correction — the IEEE quotient in practice, without the
- * device's ~30-cycle correctly rounded division sequence. */
-static float c_div(float n, float d) {
-  const float y = spt_oracle_rcp_nr(d), q = n * y;
-  return fmaf(fmaf(-q, d, n), y, q);
-}
+ * n * rcp_nr(d), within ~1 ulp of the quotient. (Round 1 added a Markstein correction to the IEEE
+ * quotient; the pdf only weights a sample, it places no geometry, and the correction cost the GPU
+ * two VALU per loop iteration.) */
+static float c_div(float n, float d) { return n * spt_oracle_rcp_nr(d); }
 
 typedef struct {
   uint64_t samples, path_rays, shadow_rays, vertices, nee_events, nee_light_hits, cosine_samples,

@@ -126,12 +126,11 @@ __device__ __forceinline__ T keep(T v) {
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-// Vec::norm :50-52 as *this * rsq(len2); exactly-unit vectors are returned unchanged.
+// Vec::norm :50-52 as *this * rsq_nr(len2) (contract, oracle fnormalize; round 1 kept exactly-unit
+// vectors unchanged with a compare + select, two VALU per normalize for a 2^-24 case).
 __device__ __forceinline__ f3 normalize3(f3 v) {
   const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
-  // exactly-unit vectors come back unchanged as v * 1 (exact): a select, not a branch
-  const float rs = keep(rsq_nr(l2));
-  const float inv = l2 == 1.0f ? 1.0f : rs;
+  const float inv = rsq_nr(l2);
   return mk(v.x * inv, v.y * inv, v.z * inv);
 }
 // operator% :56-58

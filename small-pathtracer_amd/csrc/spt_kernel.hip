@@ -527,11 +527,8 @@ constexpr int kRegions = 10;
 __device__ __forceinline__ float hit_plane_t(float n, float da, float ia, float t) {
   return fmaf(fmaf(-t, da, n), ia, t);
 }
-// n / d of the contract (oracle c_div): q = n * rcp_nr(d), one Markstein correction.
-__device__ __forceinline__ float div_mk(float n, float d) {
-  const float y = rcp_nr(d), q = n * y;
-  return fmaf(fmaf(-q, d, n), y, q);
-}
+// n / d of the contract where it only weights a sample (the NEE pdf; oracle c_div): n * rcp_nr(d).
+__device__ __forceinline__ float div_nr(float n, float d) { return n * rcp_nr(d); }
 
 __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
   return (uint32_t)(((uint64_t)n * m) >> sh);
@@ -865,7 +862,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         l_hit += lh ? 1u : 0u;
         if constexpr (!TP::SPH) ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
-        const float pdf = fabsf(div_mk(larea * d.y, t * t));            // :471
+        const float pdf = fabsf(div_nr(larea * d.y, t * t));            // :471
         const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
         const float w = lh ? pdf * brdf : 1.0f;
         T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
