@@ -290,3 +290,48 @@ def test_c5_shard_at_per_gpu_workload(spt, oracle):
                            shard_count=8)
     _, gst = _shard_at_workload(spt, oracle, spt.spheres32_scene(), p, 192, 5)
     assert gst["sphere_vertices"] > 0 and gst["vertices"] / gst["samples"] < 16
+
+
+def _random_scene(spt, rng, n_rect, n_sph, mats):
+    """The reference's room and light (:287-294) plus random axis-aligned rectangles and spheres
+    inside it, materials drawn from `mats` (DIFF / SPEC / REFR), colours in [0.1, 0.95]."""
+    prims = list(spt.cornell_scene())[:7]  # walls 0-5 and the light 6
+    for _ in range(n_rect):
+        p = spt.spt_prim()
+        p.kind = int(rng.integers(0, 3))
+        lo = {0: (1, 0), 1: (1, 0), 2: (0, 0)}[p.kind]
+        a1 = float(rng.uniform(lo[0] + 5, 80)); b1 = float(rng.uniform(lo[1] + 5, 60))
+        k = {0: rng.uniform(10, 160), 1: rng.uniform(5, 75), 2: rng.uniform(5, 95)}[p.kind]
+        p.geom[:] = [a1, a1 + float(rng.uniform(3, 25)), b1, b1 + float(rng.uniform(3, 25)), float(k)]
+        p.refl = int(rng.choice(mats))
+        p.c[:] = [float(v) for v in rng.uniform(0.1, 0.95, 3)]
+        prims.append(p)
+    for _ in range(n_sph):
+        p = spt.spt_prim()
+        p.kind = spt.SPHERE
+        r = float(rng.uniform(3, 10))
+        p.geom[:] = [r, float(rng.uniform(1 + r, 99 - r)), float(rng.uniform(r, 81.6 - r)),
+                     float(rng.uniform(r, 170 - r)), 0.0]
+        p.refl = int(rng.choice(mats))
+        p.c[:] = [float(v) for v in rng.uniform(0.1, 0.95, 3)]
+        prims.append(p)
+    return prims
+
+
+@pytest.mark.parametrize("seed,n_rect,n_sph,mats", [
+    (1, 6, 0, (0,)),        # rect-only, another topology: the generic kernel, rect tests from LDS
+    (2, 3, 9, (0,)),        # all-DIFF with spheres: the sphere kernel
+    (3, 4, 5, (0, 1, 2)),   # SPEC/REFR: the generic kernel with the refraction stack
+    (4, 0, 24, (0, 0, 1)),  # many spheres, some mirrors
+])
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_random_scenes_bit_exact(spt, oracle, seed, n_rect, n_sph, mats, nee):
+    """Randomised scenes through every kernel specialisation: image and path statistics equal to
+    the oracle's CPU statement of the contract bit for bit."""
+    rng = np.random.default_rng(seed)
+    prims = _random_scene(spt, rng, n_rect, n_sph, mats)
+    p = spt.default_params(width=40, height=30, spp=6, seed=seed, nee_prob=nee, max_depth=12)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert gst["samples"] == 40 * 30 * 6
