@@ -83,21 +83,37 @@ __global__ void census(uint32_t base, uint32_t n, unsigned long long* out) {
   if (cs) atomicAdd(out + (cs < 0 ? 4 : 5), 1ull);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // default: [1, 4); with an argument, every binade from 2^-60 to 2^4 of both signs (the
+  // reciprocal's exponent independence; rsq and sqrt are counted for positive inputs only)
+  const bool wide = argc > 1;
   unsigned long long* d = nullptr;
-  unsigned long long h[12] = {};
+  unsigned long long h[12] = {}, tot[12] = {};
   if (hipMalloc(&d, sizeof h) != hipSuccess) return 1;
-  (void)hipMemset(d, 0, sizeof h);
-  const uint32_t base = 0x3F800000u, n = 1u << 24;  // [1, 4)
-  hipLaunchKernelGGL(census, dim3((n + 255) / 256), dim3(256), 0, 0, base, n, d);
-  if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  std::printf("floats in [1,4): %u\n", n);
-  std::printf("v_rcp_f32  not correctly rounded: %llu (too small %llu, too large %llu)\n", h[0] + h[1], h[0], h[1]);
-  std::printf("v_rsq_f32  not correctly rounded: %llu (too small %llu, too large %llu)\n", h[2] + h[3], h[2], h[3]);
-  std::printf("v_sqrt_f32 not correctly rounded: %llu (too small %llu, too large %llu)\n", h[4] + h[5], h[4], h[5]);
-  std::printf("controls (must be 0): IEEE 1/x %llu, IEEE sqrtf %llu\n", h[6], h[7]);
+  uint64_t total = 0, total_pos = 0;
+  const int e_lo = wide ? -60 : 0, e_hi = wide ? 4 : 2;  // binades [2^e, 2^(e+2)) in steps of 2
+  for (int sign = 0; sign < (wide ? 2 : 1); ++sign) {
+    for (int e = e_lo; e < e_hi; e += 2) {
+      (void)hipMemset(d, 0, sizeof h);
+      const uint32_t base = (sign ? 0x80000000u : 0u) | ((uint32_t)(127 + e) << 23), n = 1u << 24;
+      hipLaunchKernelGGL(census, dim3((n + 255) / 256), dim3(256), 0, 0, base, n, d);
+      if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+      for (int k = 0; k < 12; ++k) {
+        if (sign && k >= 2 && k != 6 && k != 8) continue;  // negative x: rcp only
+        tot[k] += h[k];
+      }
+      total += n;
+      if (!sign) total_pos += n;
+    }
+  }
+  std::printf("floats checked: %llu (positive %llu), binades 2^%d .. 2^%d%s\n", (unsigned long long)total,
+              (unsigned long long)total_pos, e_lo, e_hi, wide ? ", both signs" : "");
+  std::printf("v_rcp_f32  not correctly rounded: %llu (too small %llu, too large %llu)\n", tot[0] + tot[1], tot[0], tot[1]);
+  std::printf("v_rsq_f32  not correctly rounded: %llu (too small %llu, too large %llu)\n", tot[2] + tot[3], tot[2], tot[3]);
+  std::printf("v_sqrt_f32 not correctly rounded: %llu (too small %llu, too large %llu)\n", tot[4] + tot[5], tot[4], tot[5]);
+  std::printf("controls (must be 0): IEEE 1/x %llu, IEEE sqrtf %llu\n", tot[6], tot[7]);
   std::printf("after one correction: rcp %llu, rsq (y*y) %llu, rsq (x*y) %llu, sqrt %llu not CR\n",
-              h[8], h[9], h[10], h[11]);
+              tot[8], tot[9], tot[10], tot[11]);
   (void)hipFree(d);
   return 0;
 }
