@@ -17,5 +17,5 @@ step bench 400 python -u bench.py || exit $?
 step bench_c2 120 python -u bench.py --config c2 --steps 5 --warmup 1 --no-cpu-baseline || exit $?
 step bench_c4 200 python -u bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline || exit $?
 step bench_c5 200 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline || exit $?
-step profile 600 bash scripts/profile.sh r02 || exit $?
+step profile 600 bash scripts/profile.sh ${PROF_TAG:-r02} || exit $?
 echo ALL_OK
