@@ -63,23 +63,31 @@ def host_threads() -> int:
 QUALITY_FIXTURE = os.path.join(ROOT, "tests", "golden", "ref_c3_blocks_k32.npz")
 
 
-def quality(img: np.ndarray, spp: int):
+def quality(img: np.ndarray, spp: int, extra_images=()):
     """The metric's quality half (BASELINE.json: per-channel RMSE vs the reference PPM) at C3:
     the GPU image, quantised and linearised as the reference's P3 (toInt :319-321, (v/255)^2.2),
     as 32x32-block means against the pooled block means of 16 independent runs of the reference
-    itself (oracle/_ref/smallpt_nee_xs, 1024x768 @ 64 spp each; tests/golden/ref_c3_blocks_k32.npz,
+    itself (oracle/_ref/smallpt_nee_xs, 1024x768 @ 512 spp each; tests/golden/ref_c3_blocks_k32.npz,
     made by tests/golden/make_golden.py --quality-c3). Both images are Monte-Carlo estimates, so
     the RMSE has a noise floor: the expected RMSE of two unbiased estimates at these sample counts,
-    from the spread of the 16 runs (per block: var_run * (64/spp + 1/16)); and the same RMSE
-    between the two halves of the reference runs (reference vs reference)."""
+    from the spread of the 16 runs (per block: var_run * (spp_ref/spp + 1/16)); and the same RMSE
+    between the two halves of the reference runs (reference vs reference).
+    extra_images: further GPU renders of the same config with other seeds (the bench image is
+    seed 1). Pooled with it, they give the comparison at a matched budget -- as many 512-spp runs
+    on each side -- whose noise floor is below the north star's 1e-3 tolerance. (Runs are pooled
+    rather than rendered at 16x the spp: the per-pixel clamp of :538 makes an image depend on its
+    own spp.)"""
     if not os.path.exists(QUALITY_FIXTURE):
         return None
     f = np.load(QUALITY_FIXTURE)  # plain arrays (allow_pickle=False)
     blocks, (w, h, spp_ref, k) = f["blocks"], [int(v) for v in f["shape"]]
     if img.shape != (h, w, 3):
         return None
-    v = np.floor(np.power(np.clip(img.astype(np.float64), 0, 1), 1 / 2.2) * 255 + 0.5)
-    own = ((v / 255.0) ** 2.2).reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+    def block_means(im):
+        q = np.floor(np.power(np.clip(im.astype(np.float64), 0, 1), 1 / 2.2) * 255 + 0.5)
+        return ((q / 255.0) ** 2.2).reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+
+    own = block_means(img)
     n = len(blocks)
     ref = blocks.mean(0)
     var_run = blocks.var(0, ddof=1)
@@ -87,6 +95,20 @@ def quality(img: np.ndarray, spp: int):
     floor = np.sqrt((var_run * (spp_ref / spp + 1.0 / n)).mean(axis=(0, 1)))
     half = np.sqrt(((blocks[: n // 2].mean(0) - blocks[n // 2:].mean(0)) ** 2).mean(axis=(0, 1)))
     half_floor = np.sqrt((var_run * (4.0 / n)).mean(axis=(0, 1)))
+    matched = None
+    if extra_images and spp == spp_ref:
+        gpu = np.stack([own] + [block_means(im) for im in extra_images])
+        m = len(gpu)
+        rm = np.sqrt(((gpu.mean(0) - ref) ** 2).mean(axis=(0, 1)))
+        # expected RMSE of two unbiased pooled estimates: the reference runs' and the GPU runs' own
+        # block variances (the GPU's from its m seeds)
+        fl = np.sqrt((var_run / n + gpu.var(0, ddof=1) / m).mean(axis=(0, 1)))
+        matched = {"gpu_runs": m, "reference_runs": n, "spp_each": spp,
+                   "rmse_vs_reference": [round(float(x), 6) for x in rm],
+                   "noise_floor": [round(float(x), 6) for x in fl],
+                   "ratio_to_floor": [round(float(a / b), 3) for a, b in zip(rm, fl)],
+                   "mean_diff": [round(float(x), 6) for x in (gpu.mean(0) - ref).mean(axis=(0, 1))],
+                   "seeds": f"1..{m} (Philox stream seed; the reference runs use their own seeds)"}
     return {"rmse_vs_reference": [round(float(x), 6) for x in rmse],
             "noise_floor": [round(float(x), 6) for x in floor],
             "ratio_to_floor": [round(float(a / b), 3) for a, b in zip(rmse, floor)],
@@ -94,6 +116,7 @@ def quality(img: np.ndarray, spp: int):
             "reference_halves_floor": [round(float(x), 6) for x in half_floor],
             "mean_diff": [round(float(x), 6) for x in (own - ref).mean(axis=(0, 1))],
             "rmse_vs_contract": None,
+            "matched_budget": matched,
             "space": f"linear, quantised as the reference's P3, {k}x{k}-block means, per channel (R,G,B)",
             "reference": f"{n} runs of oracle/_ref/smallpt_nee_xs at {w}x{h} @ {spp_ref} spp "
                          f"({n * spp_ref} spp pooled), tests/golden/{os.path.basename(QUALITY_FIXTURE)}"}
@@ -379,7 +402,13 @@ def main() -> None:
         if args.save_ppm:
             spt.write_ppm(args.save_ppm, img)
         writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)
-        qual = quality(img, spp) if (args.config == "c3" and world == 1) else None
+        qual = None
+        if args.config == "c3" and world == 1 and os.path.exists(QUALITY_FIXTURE):
+            # 15 more seeds of the same render (after the timed region): the matched-budget RMSE
+            extra = [spt.render(prims, cam, spt.default_params(
+                width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"], max_depth=cfg["max_depth"],
+                tile_rows=8, device=local, seed=sd_)) for sd_ in range(2, 17)]
+            qual = quality(img, spp, extra)
         if qual is not None and port is not None:
             # the bench's own rows re-rendered by the CPU contract (cpu_baseline.port): exact
             qual["rmse_vs_contract"] = 0.0 if port.get("gpu_rows_bit_exact") else None
