@@ -448,8 +448,9 @@ def main() -> None:
                          "flop_per_sample": round(float(flop.mean()) / my_samples, 1)},
             "paths": {"vertices_per_sample": round(s0["vertices"] / my_samples, 4),
                       "rays_per_sample": round((s0["path_rays"] + s0["shadow_rays"]) / my_samples, 4),
-                      "rays_traced_per_sample": round((s0["path_rays"] + s0["shadow_traced"])
-                                                      / my_samples, 4),
+                      "rays_traced_per_sample": round((s0["path_rays"] + s0["shadow_traced"]
+                                                       - s0["shadow_proven"]) / my_samples, 4),
+                      "shadow_proven_per_sample": round(s0["shadow_proven"] / my_samples, 4),
                       "misses_per_sample": round(s0["misses"] / my_samples, 4)},
             "quality": qual,
             "gather_equals_1gpu_render": gather_exact,

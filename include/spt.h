@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 2 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed */
+#define SPT_ABI_VERSION 3 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed;
+                             3: shadow_proven */
 
 typedef enum spt_status {
   SPT_OK = 0,
@@ -126,11 +127,16 @@ typedef struct spt_stats {
   uint64_t nee_light_hits; /* ... whose shadow ray hit light_id (:470-472) */
   uint64_t cosine_samples; /* cosine-weighted scatter directions drawn (:337-347) */
   uint64_t misses;         /* path rays that hit nothing (reference: x = origin, id = 0, :373-374) */
-  uint64_t shadow_traced;  /* NEE shadow rays actually traced through the scene by the kernel */
+  uint64_t shadow_traced;  /* NEE shadow rays that pass the light pre-test: the kernel resolves each
+                              of them as the nearest-hit test of :466-467 -- by tracing it, or ... */
   uint64_t sphere_vertices;/* vertices on a sphere (Sphere::normal :246-253) */
+  uint64_t shadow_proven;  /* ... of shadow_traced, those the HEAD NEE kernel proved to reach the
+                              light without a trace (exact: the trace's result is implied by the
+                              geometry; 0 in the other kernels) */
   double flop;             /* algorithmic FLOPs of the reference's work (model in spt_flops.h): every
                               shadow ray of :466 charged as a full scene test */
-  double flop_executed;    /* the same model with only the traced shadow rays charged */
+  double flop_executed;    /* the same model with only the traced shadow rays charged
+                              (shadow_traced - shadow_proven) */
   double kernel_ms;        /* device time of the render kernel (HIP events) */
 } spt_stats;
 

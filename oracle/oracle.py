@@ -150,6 +150,20 @@ def counter_render_pixels(prims, cam, params, pixels, threads: int = 0):
     return out, dict(zip(_spt.STAT_KEYS, [int(v) for v in st]))
 
 
+def proof_check(on: bool) -> None:
+    """Test hook: check the HEAD NEE kernel's early shadow-ray resolve (spt_kernel.hip
+    early_nee_proven, restated as c_early_nee_proven) against c_intersect during counter renders
+    of the HEAD scene; resets the counts."""
+    lib().spt_oracle_proof_check(1 if on else 0)
+
+
+def proof_counts() -> tuple:
+    """(claims, contradicted claims) since proof_check(True)."""
+    out = (ctypes.c_uint64 * 2)()
+    lib().spt_oracle_proof_counts(out)
+    return int(out[0]), int(out[1])
+
+
 def set_pairs(on: bool) -> None:
     """Test hook: parallel-pair rect tests on (the contract) or off (every rect on its own)."""
     lib().spt_oracle_set_pairs(1 if on else 0)

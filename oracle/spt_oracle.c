@@ -700,6 +700,33 @@ static int c_light_accepts(const c_ctx* C, fv o, fv d) {
   }
 }
 
+/* The HEAD NEE kernel's early resolve (spt_kernel.hip early_nee_proven), restated so the tests can
+ * check it against c_intersect: for the HEAD scene (rect[] :287-311, light index 6 at y = 81.5), a
+ * shadow ray (o, d) whose light test accepts and whose origin meets these conditions is claimed
+ * to have the light as its nearest hit at the light's own t (*tl). Test-only: spt_oracle_proof_*
+ * count the claims and any claim c_intersect contradicts; never changes a result. */
+static int g_proof_on;
+static uint64_t g_proof_n, g_proof_bad;
+static int c_early_nee_proven(fv o, fv d, float* tl) {
+  const float tt = (81.5f - o.y) * spt_oracle_rcp_nr(d.y);
+  const float a = fmaf(d.x, tt, o.x - 50.0f), b = fmaf(d.z, tt, o.z - 79.5f);
+  const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && (asu(tt) - 1u) < (asu(1e20f) - 1u);
+  const int room = asu(o.x) - asu(1.0f) <= asu(99.0f) - asu(1.0f) && asu(o.z) <= asu(170.0f) &&
+                   asu(o.y) < asu(81.5f);
+  const int short_box = o.y > 25.0f || (o.x < 62.99f && a < 12.99f);
+  const int tall_box = o.y > 50.0f || o.z > 62.01f;
+  *tl = tt;
+  return acc && room && short_box && tall_box;
+}
+void spt_oracle_proof_check(int on) {
+  g_proof_on = on;
+  g_proof_n = g_proof_bad = 0;
+}
+void spt_oracle_proof_counts(uint64_t out[2]) {
+  out[0] = g_proof_n;
+  out[1] = g_proof_bad;
+}
+
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   const float ix = spt_oracle_rcp_nr(d.x), iy = spt_oracle_rcp_nr(d.y), iz = spt_oracle_rcp_nr(d.z);
   float tmin = 1e20f;
@@ -985,6 +1012,14 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         dl = fnormalize(fv3(xl - x.x, P->light_y - x.y, zl - x.z));
         if (id == P->light_id || c_light_accepts(C, x, dl)) st->shadow_traced++;
         sh = c_intersect(C, x, dl, &ts, &ids);
+        if (g_proof_on) {
+          float tl;
+          if (c_early_nee_proven(x, dl, &tl)) {
+            __atomic_fetch_add(&g_proof_n, 1, __ATOMIC_RELAXED);
+            if (!sh || ids != P->light_id || asu(ts) != asu(tl))
+              __atomic_fetch_add(&g_proof_bad, 1, __ATOMIC_RELAXED);
+          }
+        }
         st->nee_events++;
         st->shadow_rays++;
         if (ids == P->light_id) {

@@ -79,7 +79,7 @@ class spt_stats(ctypes.Structure):
                 ("nee_events", ctypes.c_uint64), ("nee_light_hits", ctypes.c_uint64),
                 ("cosine_samples", ctypes.c_uint64), ("misses", ctypes.c_uint64),
                 ("shadow_traced", ctypes.c_uint64), ("sphere_vertices", ctypes.c_uint64),
-                ("flop", ctypes.c_double), ("flop_executed", ctypes.c_double),
+                ("shadow_proven", ctypes.c_uint64), ("flop", ctypes.c_double), ("flop_executed", ctypes.c_double),
                 ("kernel_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
@@ -515,7 +515,7 @@ def flop_model(stats: dict, prims: Iterable[spt_prim], executed: bool = False) -
     """include/spt_flops.h model (same as the C side): `flop`, or with executed=True
     `flop_executed` (only the traced shadow rays charged a scene test)."""
     scene = sum(19 if p.kind == SPHERE else 6 for p in prims)
-    shadow = stats["shadow_traced"] if executed else stats["shadow_rays"]
+    shadow = (stats["shadow_traced"] - stats.get("shadow_proven", 0)) if executed else stats["shadow_rays"]
     return (stats["samples"] * 40 + (stats["path_rays"] + shadow) * scene
             + stats["vertices"] * 11 + stats["sphere_vertices"] * 13
             + (stats["vertices"] - stats["samples"]) * 12

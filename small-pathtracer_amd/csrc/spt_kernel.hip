@@ -62,12 +62,15 @@ constexpr uint32_t kStSpec = 3;    // next: a path ray whose direction is alread
 constexpr uint32_t kStPath = 4;    // a path ray is set: trace it, shade its vertex
 constexpr uint32_t kStShadow = 5;  // a NEE shadow ray toward the light is set: trace, resolve
 constexpr uint32_t kStTerm = 6;    // the path ended at this vertex (within an iteration)
+constexpr uint32_t kStEarly = 7;   // a NEE shadow ray proven to reach the light (early_nee_proven)
 // Exit condition every wave reaches even if a path never terminated: a C3 wave runs ~4e3
 // iterations and a 1-GPU C5 wave ~3e6; stats[0] counts waves that hit the cap.
 constexpr uint32_t kMaxWaveIters = 1u << 26;
 // stats[]: [0] waves that hit kMaxWaveIters, [1,8) path statistics (spt_stats order), [8] shadow
-// rays traced, [9] sphere vertices, [12,32) region stats (diagnostic build)
-[[maybe_unused]] constexpr int kStatShadowTraced = 8, kStatSphereVertices = 9, kStatRegion = 12;
+// rays that passed the light pre-test, [9] sphere vertices, [10] shadow rays of those resolved
+// without a trace (early_nee_proven), [12,32) region stats (diagnostic build)
+[[maybe_unused]] constexpr int kStatShadowTraced = 8, kStatSphereVertices = 9, kStatShadowProven = 10,
+                               kStatRegion = 12;
 
 // 64-byte device primitive. rect: w1..w5 = k, b1, b2, c1, c2 (in-plane bounds of the two free
 // axes in (x,y,z) order); sphere: w1..w5 = px, py, pz, rad^2, 1/rad.
@@ -338,13 +341,13 @@ __device__ __forceinline__ void test_group(GT g, int n_rt, const Ray6& r, uint32
   }
 }
 
-struct RectHit { float tt; bool inb; };
+struct RectHit { float tt; bool inb; float a; };  // a: first in-plane offset from the centre
 template <class GP>
 __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   const float tt = (g->k - r.oa) * r.ia;
   const float a = fmaf(r.db, tt, r.ob - g->ma), b = fmaf(r.dc, tt, r.oc - g->mb);
   const bool ia = fabsf(a) <= g->ha, ib = fabsf(b) <= g->hb;
-  return RectHit{tt, (bool)((int)ia & (int)ib)};
+  return RectHit{tt, (bool)((int)ia & (int)ib), a};
 }
 
 struct alignas(16) SphLds { float px, py, pz, rad2; };  // a narrow sphere's LDS copy
@@ -509,6 +512,32 @@ __device__ __forceinline__ bool light_accepts(const SPT_CONST KParams* P, const 
   }
 }
 
+// Early NEE resolve (the HEAD NEE kernel: compile-time HEAD geometry, the reference's light
+// constants, black light). A shadow ray (x, dl) whose light test accepts (t_L, crossing
+// x_L = 50 + a) cannot meet any primitive before the light when x satisfies the conditions below,
+// so intersect() (:323-335, oracle c_intersect) would return the light with t = t_L, bit for bit:
+// the lane resolves it in the iteration that sampled it instead of tracing it in the next one.
+//   * room: 1 <= x <= 99, 0 <= z <= 170, 0 <= y < 81.5. Each room pair then selects the plane
+//     ahead of the ray, never the one the vertex lies on (a vertex rounded outside its wall keeps
+//     its self-hit: traced), and that plane lies >= 31 units beyond the light crossing in x
+//     (the light spans x 32..68), >= 63 in z (z 63..96); the ceiling is 0.1 above the light plane.
+//   * short box (x, z in [63, 88], y <= 25): y > 25 (every face's y bound fails for t > 0, the
+//     top's t < 0), or x < 62.99 and x_L < 62.99 (x stays below 63 along the segment).
+//   * tall box (x in [12, 42], z in [32, 62], y <= 50): y > 50, or z > 62.01 (z stays above 62
+//     along the segment, since the light's z >= 63).
+// Faces crossed beyond t_L fail their y bounds (y > 81.5 there) or lose to the light on t. The
+// oracle restates the predicate and checks it against its own intersect() (spt_oracle_proof_*,
+// tests/test_oracle.py); it covers ~68 % of the shadow rays that reach the light at C3.
+__device__ __forceinline__ bool early_nee_proven(f3 x, float a_light) {
+  const int room = (int)(__float_as_uint(x.x) - __float_as_uint(1.0f) <=
+                        __float_as_uint(99.0f) - __float_as_uint(1.0f)) &
+                   (int)(__float_as_uint(x.z) <= __float_as_uint(170.0f)) &
+                   (int)(__float_as_uint(x.y) < __float_as_uint(81.5f));  // +0 <= v: no sign bit
+  const int short_box = (int)(x.y > 25.0f) | ((int)(x.x < 62.99f) & (int)(a_light < 12.99f));
+  const int tall_box = (int)(x.y > 50.0f) | (int)(x.z > 62.01f);
+  return (room & short_box & tall_box) != 0;
+}
+
 // Diagnostic build (-DSPT_REGION_STATS): per code region, wave executions and active lanes,
 // counted with wave-uniform SALU ballots and flushed once per wave to stats[8 + 2*region].
 #ifdef SPT_REGION_STATS
@@ -667,6 +696,15 @@ render_kernel(const KParams* __restrict__ Pg) {
   // NEE events need no counter in the HEAD NEE kernels: with NEE always on and no SPEC/REFR, every
   // non-terminal vertex takes one (nee_events = vertices - samples, added by the host).
   constexpr bool kNeeByIdentity = CF::NEE == 1 && !TP::MAT;
+  // Early NEE resolve (early_nee_proven): the HEAD NEE kernel only. The shadow-ray resolve then
+  // runs after the shading block, for the rays traced in this iteration and the proven ones.
+#ifdef SPT_NO_EARLY_NEE  // A/B builds only
+  constexpr bool kEarlyNee = false;
+#else
+  constexpr bool kEarlyNee = TP::CONSTGEO && !TP::MAT && !TP::SPH && CF::NEE == 1 &&
+                             CF::BLACK == 1 && CF::LREF == 1 && CF::MAXD0 == 1;
+#endif
+  uint32_t l_early = 0;  // shadow rays resolved early (stats[kStatShadowProven])
   uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
   // Shadow rays traced (NEE samples that passed light_accepts()): per lane in the rect kernels,
   // wave-uniform in the sphere kernels (a ballot of the kStShadow lanes at the convergent point
@@ -854,7 +892,8 @@ render_kernel(const KParams* __restrict__ Pg) {
       //    the light is the next vertex (shaded in the common block below, T = T*f*weight); else the
       //    cosine sample follows (:468-469, T = T*f). The weight is computed for every shadow lane
       //    and applied as T*1 (exact) where the light is not reached: no branch.
-      if (ls == kStShadow) {
+      const bool traced_shadow = ls == kStShadow;
+      if (!kEarlyNee && ls == kStShadow) {
         SPT_REGION(6);
         const SPT_CONST KParams* D = cptr(Pg);
         const bool lh = id == light_id_of<CF>(D);
@@ -1039,13 +1078,46 @@ render_kernel(const KParams* __restrict__ Pg) {
             if constexpr (!kNeeByIdentity) l_nee += term ? 0u : 1u;
             const SPT_CONST SceneGeo* G2 = TP::CONSTGEO ? nullptr : cptr(D->geo);
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
-            const bool la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
+            bool la, early = false;
+            if constexpr (kEarlyNee) {  // the light's own test (light_accepts), keeping t and a
+              const RectHit h = rect_eval(CornellRectPtr{kCornellLightPos},
+                                          Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
+              la = h.inb & (tkey(h.tt) < tkey(1e20f));
+              early = la & early_nee_proven(x, h.a);
+              t = early ? h.tt : t;  // the t the trace would return (the light's test, same bits)
+            } else {
+              la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
+            }
             const bool cand = (id == light_id_of<CF>(D)) | la;
             d = dl;  // a rejected lane generates its cosine direction next iteration anyway
-            nxt = cand ? kStShadow : kStCos;
+            nxt = early ? kStEarly : (cand ? kStShadow : kStCos);
           }
         }
         ls = term ? kStTerm : nxt;
+      }
+      // 5') the HEAD NEE kernel resolves shadow rays here, after the shading block: the ones traced
+      //    in this iteration and the ones early_nee_proven() has just resolved (t = the light's t,
+      //    the same bits the trace returns). Same arithmetic as 5); the light is black, so a ray
+      //    that reaches it shades the light vertex as L += (T*w)*e and ends the path (RR with
+      //    p == 0, :448), which is all the common vertex block would do there.
+      if constexpr (kEarlyNee) {
+        if (traced_shadow || ls == kStEarly) {
+          SPT_REGION(6);
+          const bool ea = ls == kStEarly;
+          const bool lh = ea | (id == kRefLightId);
+          if (lh) SPT_REGION(7);
+          l_hit += lh ? 1u : 0u;
+          l_early += ea ? 1u : 0u;
+          ++l_shadow;
+          const float pdf = fabsf(div_nr(kRefLarea * d.y, t * t));          // :471
+          const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
+          const float w = lh ? pdf * brdf : 1.0f;
+          T = mk(T.x * w, T.y * w, T.z * w);
+          const DevPrim& H = s_prims[kRefLightId];
+          const f3 Le = mk(fmaf(T.x, H.ex, L.x), fmaf(T.y, H.ey, L.y), fmaf(T.z, H.ez, L.z));
+          L = mk(lh ? Le.x : L.x, lh ? Le.y : L.y, lh ? Le.z : L.z);
+          ls = lh ? kStTerm : kStCos;
+        }
       }
       // 7) path end: accumulate this sample (:536-538) and start the next one.
       if (ls == kStTerm) {
@@ -1155,6 +1227,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       }
       if constexpr (TP::SPH)
         if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)s_nsph[threadIdx.x / 64]);
+      if constexpr (kEarlyNee) atomicAdd(st + kStatShadowProven, (unsigned long long)l_early);
     }
   }
 }
@@ -1678,13 +1751,15 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   out->misses = h[7];
   out->shadow_traced = h[kStatShadowTraced];
   out->sphere_vertices = h[kStatSphereVertices];
+  out->shadow_proven = h[kStatShadowProven];
   if (c->nee_by_identity) {  // HEAD NEE kernels: one NEE event per non-terminal vertex
     out->nee_events = out->vertices - out->samples;
     out->shadow_rays = out->nee_events;
   }
   // FLOP model (include/spt_flops.h): scene cost per ray from the primitive mix. `flop` charges
   // a full scene test for every shadow ray of the reference (:466); `flop_executed` only for the
-  // shadow rays the kernel traced (the others are rejected exactly by the light pre-test).
+  // shadow rays the kernel traced (the others are rejected exactly by the light pre-test or
+  // resolved by early_nee_proven()).
   const double scene = c->scene_flop;
   const double common = (double)out->samples * SPT_FLOP_SAMPLE +
                         (double)out->path_rays * scene + (double)out->vertices * SPT_FLOP_VERTEX +
@@ -1694,7 +1769,7 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
                         (double)out->nee_events * SPT_FLOP_NEE +
                         (double)out->nee_light_hits * SPT_FLOP_NEE_HIT;
   out->flop = common + (double)out->shadow_rays * scene;
-  out->flop_executed = common + (double)out->shadow_traced * scene;
+  out->flop_executed = common + (double)(out->shadow_traced - out->shadow_proven) * scene;
   out->kernel_ms = ms;
   c->pending = false;
   return SPT_OK;

@@ -320,6 +320,7 @@ extern "C" spt_status spt_render_multi(const spt_prim* prims, int32_t n_prims, c
     tot.vertices += s.vertices; tot.nee_events += s.nee_events; tot.nee_light_hits += s.nee_light_hits;
     tot.cosine_samples += s.cosine_samples; tot.misses += s.misses;
     tot.shadow_traced += s.shadow_traced; tot.sphere_vertices += s.sphere_vertices;
+    tot.shadow_proven += s.shadow_proven;
     tot.flop += s.flop; tot.flop_executed += s.flop_executed;
     tot.kernel_ms = std::max(tot.kernel_ms, s.kernel_ms);
   }

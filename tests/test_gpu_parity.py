@@ -231,6 +231,25 @@ def test_full_size_configs_rows_bit_exact(spt, oracle, cfg):
     _assert_exact(gpu[rows], cpu)
 
 
+@pytest.mark.parametrize("seed", [1, 5])
+def test_early_nee_resolve_matches_oracle_proof(spt, oracle, seed):
+    """The HEAD NEE kernel resolves the shadow rays early_nee_proven() covers without tracing them.
+    The image and path statistics stay bit-exact, and the number of rays it resolved that way
+    equals the oracle's count of the same claims, none of which its own intersect contradicts."""
+    p = spt.default_params(width=256, height=192, spp=32, seed=seed)
+    oracle.proof_check(True)
+    try:
+        gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    _assert_exact(gpu, cpu)
+    for k in spt.STAT_KEYS:
+        assert gst[k] == cst[k], k
+    assert bad == 0 and claims > 0.4 * cst["nee_light_hits"], (claims, bad, cst["nee_light_hits"])
+    assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
+
+
 def test_c4_geometry_pixel_indices_beyond_2p24(spt, oracle):
     """4096x4096 (configs[3] image size) at 1 spp: pixel counters above 2^24 still match."""
     w = h = 4096

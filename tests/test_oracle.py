@@ -203,6 +203,27 @@ def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
     assert np.array_equal(a, b) and sa == sb
 
 
+@pytest.mark.parametrize("pairs", [True, False])
+def test_early_nee_resolve_proof_holds(oracle, pairs):
+    """The HEAD NEE kernel's early shadow-ray resolve (spt_kernel.hip early_nee_proven) claims the
+    light is the nearest hit at the light's own t. Every claim is checked against the contract's
+    intersect (and with pairs=False against the per-rect tests of :323-335 as written): none is
+    contradicted, and the claims cover well over half of the shadow rays that reach the light."""
+    prims = oracle.scene_cornell()
+    w, h, spp = (256, 192, 48) if pairs else (192, 144, 32)
+    p = oracle.default_params(width=w, height=h, spp=spp, seed=11)
+    oracle.set_pairs(pairs)
+    oracle.proof_check(True)
+    try:
+        _, st = oracle.counter_render(prims, oracle.camera(w / h), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+        oracle.set_pairs(True)
+    assert bad == 0, (claims, bad)
+    assert claims > 0.55 * st["nee_light_hits"], (claims, st["nee_light_hits"])
+
+
 def test_counter_mode_thread_invariance(oracle):
     prims = oracle.scene_cornell()
     p = oracle.default_params(width=40, height=24, spp=8, seed=3)
