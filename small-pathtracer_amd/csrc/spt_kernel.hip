@@ -13,6 +13,9 @@
 //     reference's HEAD scene is compiled into the instruction stream, other scenes' rect tests are
 //     staged once per block into LDS (broadcast reads) and their spheres read with wave-uniform
 //     scalar loads; the per-lane lookups of the hit primitive (material) come from LDS;
+//   * a NEE shadow ray is traced only if the light's own test accepts it; in the reference's room
+//     the HEAD NEE kernel resolves most of those at once, where an exact geometric predicate
+//     proves that nothing lies between the vertex and the light (early_nee_proven);
 //   * Philox4x32-10 counter RNG keyed by (seed; pixel, sample, vertex, stream);
 //   * per-pixel accumulation in 1.31 fixed point with 64-bit integer atomics: exact, independent
 //     of unit size, lane order, queue order, stealing and GPU count.
