@@ -894,7 +894,8 @@ render_kernel(const KParams* __restrict__ Pg) {
       // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467). Then
       //    the light is the next vertex (shaded in the common block below, T = T*f*weight); else the
       //    cosine sample follows (:468-469, T = T*f). The weight is computed for every shadow lane
-      //    and applied as T*1 (exact) where the light is not reached: no branch.
+      //    and applied as T*1 (exact) where the light is not reached: no branch. (The HEAD NEE
+      //    kernel resolves in 5') below instead, after the shading block.)
       const bool traced_shadow = ls == kStShadow;
       if (!kEarlyNee && ls == kStShadow) {
         SPT_REGION(6);
