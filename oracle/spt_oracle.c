@@ -705,7 +705,8 @@ static int c_light_accepts(const c_ctx* C, fv o, fv d) {
  * shadow ray (o, d) whose light test accepts and whose origin meets these conditions is claimed
  * to have the light as its nearest hit at the light's own t (*tl). Test-only: spt_oracle_proof_*
  * count the claims and any claim c_intersect contradicts; never changes a result. */
-static int g_proof_on;
+static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0 - 1 in the HEAD room */
+static float g_proof_y0;
 static uint64_t g_proof_n, g_proof_bad;
 static int c_early_nee_proven(fv o, fv d, float* tl) {
   const float tt = (81.5f - o.y) * spt_oracle_rcp_nr(d.y);
@@ -716,10 +717,12 @@ static int c_early_nee_proven(fv o, fv d, float* tl) {
   const int short_box = o.y > 25.0f || (o.x < 62.99f && a < 12.99f);
   const int tall_box = o.y > 50.0f || o.z > 62.01f;
   *tl = tt;
+  if (g_proof_on == 2) return acc && room && o.y > g_proof_y0; /* spt_kernel.hip early_room_proven */
   return acc && room && short_box && tall_box;
 }
-void spt_oracle_proof_check(int on) {
+void spt_oracle_proof_check(int on, float y0) {
   g_proof_on = on;
+  g_proof_y0 = y0;
   g_proof_n = g_proof_bad = 0;
 }
 void spt_oracle_proof_counts(uint64_t out[2]) {

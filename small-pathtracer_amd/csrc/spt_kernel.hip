@@ -143,6 +143,9 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // light" — an occlusion query without id bookkeeping.
   int light_black, light_kind, light_pos;
   int scatter_uniform;  // SPT_FLAG_UNIFORM_SCATTER
+  // Sphere NEE kernel: vertices above early_y0 (every sphere's top + 1) in the HEAD room resolve
+  // their light-accepted shadow rays early (early_room_proven); +inf when the host cannot prove it
+  float early_y0;
   unsigned long long* accum;  // [n_local_pix][3] 32.32 fixed point
   uint32_t* queue;            // [0] = next unit
   unsigned long long* stats;  // [8]
@@ -218,6 +221,8 @@ struct Cfg {
 using CfgRuntime = Cfg<-1, -1, -1, -1, -1, -1>;
 using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
 using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1>;  // C2: cosine-weighted only
+// Sphere scenes with the reference's NEE estimator and black light (C5): early NEE resolve
+using CfgSphNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, -1, -1, -1, 1>;
 // The LREF constants (the host checks spt_params against them before it picks an LREF kernel).
 constexpr int kRefLightId = 6, kRefRrDepth = 5;
 constexpr float kRefLx0 = 32.0f, kRefLz0 = 63.0f, kRefLy = 81.6f, kRefLarea = 1296.0f;
@@ -531,11 +536,21 @@ __device__ __forceinline__ bool light_accepts(const SPT_CONST KParams* P, const 
 // Faces crossed beyond t_L fail their y bounds (y > 81.5 there) or lose to the light on t. The
 // oracle restates the predicate and checks it against its own intersect() (spt_oracle_proof_*,
 // tests/test_oracle.py); it covers ~68 % of the shadow rays that reach the light at C3.
+__device__ __forceinline__ int early_room_ok(f3 x) {
+  return (int)(__float_as_uint(x.x) - __float_as_uint(1.0f) <=
+               __float_as_uint(99.0f) - __float_as_uint(1.0f)) &
+         (int)(__float_as_uint(x.z) <= __float_as_uint(170.0f)) &
+         (int)(__float_as_uint(x.y) < __float_as_uint(81.5f));  // +0 <= v: no sign bit
+}
+// Sphere scenes in the HEAD room (the sphere NEE kernel, C5): with every sphere's top below
+// y0 - 1, a vertex above y0 whose shadow ray goes up (dl.y > 0) cannot meet a sphere for t > 0:
+// the real intersections lie at t <= -1, and the fp32 quadratic's rounding (|det| error < 0.02
+// for |op| < 200) cannot lift a root above the 2e-3 epsilon. The room as above.
+__device__ __forceinline__ bool early_room_proven(f3 x, float y0) {
+  return (early_room_ok(x) & (int)(x.y > y0)) != 0;
+}
 __device__ __forceinline__ bool early_nee_proven(f3 x, float a_light) {
-  const int room = (int)(__float_as_uint(x.x) - __float_as_uint(1.0f) <=
-                        __float_as_uint(99.0f) - __float_as_uint(1.0f)) &
-                   (int)(__float_as_uint(x.z) <= __float_as_uint(170.0f)) &
-                   (int)(__float_as_uint(x.y) < __float_as_uint(81.5f));  // +0 <= v: no sign bit
+  const int room = early_room_ok(x);
   const int short_box = (int)(x.y > 25.0f) | ((int)(x.x < 62.99f) & (int)(a_light < 12.99f));
   const int tall_box = (int)(x.y > 50.0f) | (int)(x.z > 62.01f);
   return (room & short_box & tall_box) != 0;
@@ -621,6 +636,9 @@ template <class TP, class CF>
 #define SPT_NUM_SGPR 80
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(SPT_NUM_SGPR)))
+// The sphere kernels allocate for 8 waves/SIMD explicitly: the NEE-specialised one otherwise takes
+// 65 VGPRs (7 waves); with the hint it fits 64 with no spills (the others are unaffected)
+__attribute__((amdgpu_waves_per_eu(TP::SPH && !TP::MAT && !TP::WIDE ? 8 : 1)))
 render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
@@ -637,6 +655,9 @@ render_kernel(const KParams* __restrict__ Pg) {
   // lanes); one LDS add per wave (the atomic optimizer folds the lanes) keeps it out of the VGPRs.
   __shared__ uint32_t s_nsph[TP::SPH ? kBlock / 64 : 1];
   if (TP::SPH && threadIdx.x < kBlock / 64) s_nsph[threadIdx.x] = 0;
+  // Shadow rays resolved early, per wave, in the sphere kernels (same reason: no VGPR counter)
+  __shared__ uint32_t s_nearly[TP::SPH ? kBlock / 64 : 1];
+  if (TP::SPH && threadIdx.x < kBlock / 64) s_nearly[threadIdx.x] = 0;
   {
     const SPT_CONST KParams* P = cptr(Pg);
     const SPT_CONST SceneGeo* G = cptr(P->geo);
@@ -707,6 +728,10 @@ render_kernel(const KParams* __restrict__ Pg) {
   constexpr bool kEarlyNee = TP::CONSTGEO && !TP::MAT && !TP::SPH && CF::NEE == 1 &&
                              CF::BLACK == 1 && CF::LREF == 1 && CF::MAXD0 == 1;
 #endif
+  // The sphere NEE kernel (C5): the same early resolve with the sphere-scene predicate.
+  constexpr bool kEarlySph = !kEarlyNee && TP::SPH && !TP::MAT && !TP::WIDE && CF::NEE == 1 &&
+                             CF::BLACK == 1 && CF::LREF == 1;
+  constexpr bool kEarly = kEarlyNee || kEarlySph;
   uint32_t l_early = 0;  // shadow rays resolved early (stats[kStatShadowProven])
   uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
   // Shadow rays traced (NEE samples that passed light_accepts()): per lane in the rect kernels,
@@ -897,7 +922,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       //    and applied as T*1 (exact) where the light is not reached: no branch. (The HEAD NEE
       //    kernel resolves in 5') below instead, after the shading block.)
       const bool traced_shadow = ls == kStShadow;
-      if (!kEarlyNee && ls == kStShadow) {
+      if (!kEarly && ls == kStShadow) {
         SPT_REGION(6);
         const SPT_CONST KParams* D = cptr(Pg);
         const bool lh = id == light_id_of<CF>(D);
@@ -1089,6 +1114,12 @@ render_kernel(const KParams* __restrict__ Pg) {
               la = h.inb & (tkey(h.tt) < tkey(1e20f));
               early = la & early_nee_proven(x, h.a);
               t = early ? h.tt : t;  // the t the trace would return (the light's test, same bits)
+            } else if constexpr (kEarlySph) {  // the uploaded light rect (XZ, host-checked)
+              const RectHit h = rect_eval(G2->rect + D->light_pos,
+                                          Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
+              la = h.inb & (tkey(h.tt) < tkey(1e20f));
+              early = la & early_room_proven(x, D->early_y0);
+              t = early ? h.tt : t;
             } else {
               la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
             }
@@ -1104,15 +1135,19 @@ render_kernel(const KParams* __restrict__ Pg) {
       //    the same bits the trace returns). Same arithmetic as 5); the light is black, so a ray
       //    that reaches it shades the light vertex as L += (T*w)*e and ends the path (RR with
       //    p == 0, :448), which is all the common vertex block would do there.
-      if constexpr (kEarlyNee) {
+      if constexpr (kEarly) {
         if (traced_shadow || ls == kStEarly) {
           SPT_REGION(6);
           const bool ea = ls == kStEarly;
           const bool lh = ea | (id == kRefLightId);
           if (lh) SPT_REGION(7);
           l_hit += lh ? 1u : 0u;
-          l_early += ea ? 1u : 0u;
-          ++l_shadow;
+          if constexpr (TP::SPH) {  // (sphere kernels ballot-count the traced ones)
+            if (ea) atomicAdd(&s_nearly[threadIdx.x / 64], 1u);
+          } else {
+            l_early += ea ? 1u : 0u;
+            ++l_shadow;
+          }
           const float pdf = fabsf(div_nr(kRefLarea * d.y, t * t));          // :471
           const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
           const float w = lh ? pdf * brdf : 1.0f;
@@ -1232,6 +1267,13 @@ render_kernel(const KParams* __restrict__ Pg) {
       if constexpr (TP::SPH)
         if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)s_nsph[threadIdx.x / 64]);
       if constexpr (kEarlyNee) atomicAdd(st + kStatShadowProven, (unsigned long long)l_early);
+      if constexpr (kEarlySph) {
+        if (lane == 0) {
+          const unsigned long long ne = s_nearly[threadIdx.x / 64];
+          atomicAdd(st + kStatShadowProven, ne);
+          atomicAdd(st + kStatShadowTraced, ne);
+        }
+      }
     }
   }
 }
@@ -1269,12 +1311,13 @@ static spt_status fail(spt_status s, const std::string& msg) {
 // Kernel variants, from the most general to the most specialised (SPT_FLAG_KERNEL_LEVEL caps the
 // level).
 using RenderFn = void (*)(const KParams*);
-enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE, KV_COUNT };
+enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
+       KV_SPHDIFF_NEE, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
     render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>,
-    render_kernel<TopoGenericWide, CfgRuntime>};
+    render_kernel<TopoGenericWide, CfgRuntime>, render_kernel<TopoSphDiff, CfgSphNee>};
 
 struct spt_context {
   int device = 0;
@@ -1630,7 +1673,32 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   else if (cconst) kv = KV_CONST;
   else if (cornell) kv = KV_CORNELL;
   else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
-    kv = KV_SPHDIFF;
+    kv = kcap >= 3 && K.light_black && lref && p->nee_prob >= 1.0f &&
+                 p->light_mode == SPT_LIGHT_GLIBC_WRAP && light_pos >= 0 &&
+                 prims[p->light_id].kind == SPT_RECT_XZ
+             ? KV_SPHDIFF_NEE
+             : KV_SPHDIFF;
+  // The sphere NEE kernel's early resolve needs the HEAD room (rect[] :287-294, light at index 6)
+  // as prims 0..6, nothing else but narrow spheres, and a threshold above every sphere's top
+  // (early_room_proven); otherwise it stays off (+inf) and every shadow ray is traced.
+  K.early_y0 = INFINITY;
+  if (kv == KV_SPHDIFF_NEE && n_prims > 7 && g.n_sph_wide == 0) {
+    spt_prim head[17];
+    int32_t nh = 0;
+    bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
+    for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
+    double top = -INFINITY;
+    for (int i = 7; ok && i < n_prims; ++i) {
+      ok = prims[i].kind == SPT_SPHERE && std::isfinite(prims[i].geom[0]) &&
+           std::isfinite(prims[i].geom[2]);
+      top = std::max(top, prims[i].geom[2] + std::fabs(prims[i].geom[0]));
+    }
+    if (ok && top + 1.0 < 81.0) {
+      float y0 = (float)(top + 1.0);
+      if ((double)y0 < top + 1.0) y0 = std::nextafter(y0, INFINITY);
+      K.early_y0 = y0;
+    }
+  }
   // Unit size: ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured
   // 25.0 ms vs 26.0 ms at 8 units/lane and 27.8 ms at 2); never changes results (integer
   // accumulation).
@@ -1696,7 +1764,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 #ifdef SPT_WAVE_TIMES
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
-  c->nee_by_identity = kv == KV_CONST_NEE;
+  c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE;
   const int grid = c->n_cu * c->bpc[kv];
   *c->h_kp = K;
   SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));

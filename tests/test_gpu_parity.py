@@ -250,6 +250,24 @@ def test_early_nee_resolve_matches_oracle_proof(spt, oracle, seed):
     assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
 
 
+def test_early_nee_resolve_spheres_matches_oracle_proof(spt, oracle):
+    """The sphere NEE kernel (C5's scene and estimator, depth cap 16) resolves the shadow rays of
+    vertices above every sphere's top + 1 (y0 = 13) early: bit-exact image and statistics, and the
+    same count as the oracle's claims, none contradicted."""
+    p = spt.default_params(width=128, height=96, spp=16, seed=9, max_depth=16)
+    oracle.proof_check(True, sphere_y0=13.0)
+    try:
+        gpu, gst, cpu, cst = _render_both(spt, oracle, spt.spheres32_scene(), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    _assert_exact(gpu, cpu)
+    for k in spt.STAT_KEYS:
+        assert gst[k] == cst[k], k
+    assert bad == 0 and claims > 0, (claims, bad)
+    assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
+
+
 def test_c4_geometry_pixel_indices_beyond_2p24(spt, oracle):
     """4096x4096 (configs[3] image size) at 1 spp: pixel counters above 2^24 still match."""
     w = h = 4096

@@ -224,6 +224,21 @@ def test_early_nee_resolve_proof_holds(oracle, pairs):
     assert claims > 0.55 * st["nee_light_hits"], (claims, st["nee_light_hits"])
 
 
+def test_early_nee_resolve_proof_holds_spheres(oracle, spt):
+    """The sphere NEE kernel's early resolve (early_room_proven: the HEAD room, vertices above
+    every sphere's top + 1 = 13 in the C5 scene) against the contract's intersect, depth cap 16."""
+    prims = spt.spheres32_scene()
+    p = oracle.default_params(width=160, height=120, spp=32, seed=5, max_depth=16)
+    oracle.proof_check(True, sphere_y0=13.0)
+    try:
+        _, st = oracle.counter_render(prims, oracle.camera(160 / 120), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    assert bad == 0, (claims, bad)
+    assert claims > 0.3 * st["nee_light_hits"], (claims, st["nee_light_hits"])
+
+
 def test_counter_mode_thread_invariance(oracle):
     prims = oracle.scene_cornell()
     p = oracle.default_params(width=40, height=24, spp=8, seed=3)
