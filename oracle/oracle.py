@@ -232,3 +232,9 @@ def sincos2pi(xi: float):
 
 def threads() -> int:
     return lib().spt_oracle_threads()
+
+
+def set_unit_dirs(mode) -> None:
+    """Test hook: None = the contract (unit directions iff the scene has a sphere or a REFR prim),
+    True/False = force normalised / free-scale directions (diagnostics only)."""
+    lib().spt_oracle_set_unit_dirs(-1 if mode is None else (1 if mode else 0))

@@ -476,6 +476,23 @@ float spt_oracle_rsq_nr(float x) {
   }
   return y;
 }
+/* The same reciprocal square root with two Newton steps (relative error < 5e-6): the free-scale
+ * contract's normalize (c_unit_dirs), where a direction need only be unit to ~1e-5. */
+float spt_oracle_rsq_nr2(float x) {
+  float y = asf(0x5F375A86u - (asu(x) >> 1));
+  const float h = 0.5f * x;
+  int i;
+  for (i = 0; i < 2; i++) {
+    const float hy = h * y;
+    y = y * fmaf(-hy, y, 1.5f);
+  }
+  return y;
+}
+static inline fv fnormalize2(fv v) {
+  const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+  const float inv = spt_oracle_rsq_nr2(l2);
+  return fv3(v.x * inv, v.y * inv, v.z * inv);
+}
 /* Vec::norm :50-52 as v * rsq_nr(len2). (Round 1 returned exactly-unit vectors unchanged, as the
  * reference's fp64 1/sqrt(1) does; rsq_nr(1) is 1 - 2^-24, and the select cost every normalize two
  * VALU on the GPU for vectors that occur with probability ~2^-24.) */
@@ -580,7 +597,39 @@ typedef struct {
   uint32_t key[2];
   const c_test* tests; /* rect tests in contract order (c_build_tests) */
   int n_tests;
+  int unit;     /* c_unit_dirs: 1 = unit directions, 0 = the free-scale contract */
+  float nee_c;  /* free-scale NEE weight constant: light_area / pi, rounded once */
 } c_ctx;
+
+/* Contract: the precision of ray directions. Unit directions (normalised with rsq_nr) where
+ * something needs |d| = 1 to fp32 accuracy: the sphere quadratic (:229-239 assumes |d| = 1) and
+ * the REFR Fresnel terms (:485-491 treat d.nl as a cosine). Otherwise (rectangles, DIFF/SPEC) the
+ * FREE-SCALE contract:
+ *  - path directions (camera ray, cosine sample) are normalised with two Newton steps
+ *    (rsq_nr2, |d| = 1 within 5e-6). They must stay unit to ~1e-4: the self-hit / leak rate of the
+ *    rect tests depends on |d| (measured, 256x192 @ 64 cosine-only: misses per sample 0.458 at
+ *    |d| = 1 +- 1e-3, but 0.67 at |d| = 0.75 or 1.5 and 0.71 at 1.25), as on the reference's fp64
+ *    unit vectors;
+ *  - the NEE shadow vector light_vec - hit (:367) is not normalised at all: the shadow ray only
+ *    asks whether its nearest hit is the light (:466-467), which does not depend on the scale, and
+ *    the weight :471-472 is written without the length (c_nee_weight). */
+static int c_unit_dirs(const spt_prim* s, int n) {
+  int i;
+  for (i = 0; i < n; i++)
+    if (s[i].kind == SPT_SPHERE || s[i].refl == SPT_REFR) return 1;
+  return 0;
+}
+static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T);
+static int g_unit_override = -1; /* test hook: -1 = the contract (c_unit_dirs), 0/1 = forced */
+void spt_oracle_set_unit_dirs(int mode) { g_unit_override = mode; }
+static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n, const spt_params* P,
+                       c_test* CT) {
+  C->prims = CP; C->n = n; C->P = P; C->key[0] = SPT_PHILOX_KEY0; C->key[1] = SPT_PHILOX_KEY1;
+  C->n_tests = c_build_tests(CP, n, P->light_id, CT);
+  C->tests = CT;
+  C->unit = g_unit_override >= 0 ? g_unit_override : c_unit_dirs(prims, n);
+  C->nee_c = (float)((double)P->light_area / 3.14159265358979323846);
+}
 
 /* Contract: the rect test list. Kinds in the order XY, XZ, YZ; inside a kind, rectangles in index
  * order, each paired with the first later unpaired rectangle of its kind whose (ma, ha, mb, hb) are
@@ -787,7 +836,7 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
 
 /* random_scattering in the contract: cosine (:340-347), or with `uniform` the commented-out
    uniform hemisphere (:352-359): radial sqrt(r2*(2-r2)) and normal component (1-r2). */
-static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
+static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform, int unit) {
   const float xi2 = u01(rb);
   float s, c;
   fv a, u, v;
@@ -795,13 +844,14 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
   spt_oracle_disk_dir(ra, &c, &s); /* the azimuth r1 = 2*pi*xi1 of :343 */
   if (uniform) {
     const float m = xi2 * (2.0f - xi2);
-    r2s = m * spt_oracle_rsq_nr(m);
+    r2s = m * (unit ? spt_oracle_rsq_nr(m) : spt_oracle_rsq_nr2(m));
     s1 = 1.0f - xi2;
   } else {
     /* (cos, sin) * sqrt(r2) and sqrt(1 - r2) (:343-347) scaled by 1 / sqrt(1 - r2): the direction
        is normalized below anyway, so the contract takes R = sqrt(r2 / (1 - r2)) with ONE rsqrt,
        R = r2 * rsq(r2 * (1 - r2)), and a normal component of exactly 1. */
-    r2s = xi2 * spt_oracle_rsq_nr(xi2 * (1.0f - xi2));
+    const float q = xi2 * (1.0f - xi2);
+    r2s = xi2 * (unit ? spt_oracle_rsq_nr(q) : spt_oracle_rsq_nr2(q));
     s1 = 1.0f;
   }
   cr = c * r2s;
@@ -814,16 +864,20 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform) {
        nl = (sx,0,0) -> (sx*s1, sr, -sx*cr); (0,sy,0) -> (sr, sy*s1, sy*cr);
        (0,0,sz) -> (sr, -sz*cr, sz*s1). Same values as the general formula below up to the sign
        of exact zeros. */
-    if (nl.x != 0.0f) return fnormalize(fv3(nl.x * s1, sr, -(nl.x * cr)));
-    if (nl.y != 0.0f) return fnormalize(fv3(sr, nl.y * s1, nl.y * cr));
-    return fnormalize(fv3(sr, -(nl.z * cr), nl.z * s1));
+    fv r;
+    if (nl.x != 0.0f) r = fv3(nl.x * s1, sr, -(nl.x * cr));
+    else if (nl.y != 0.0f) r = fv3(sr, nl.y * s1, nl.y * cr);
+    else r = fv3(sr, -(nl.z * cr), nl.z * s1);
+    return unit ? fnormalize(r) : fnormalize2(r);
   }
   a = fabsf(nl.x) > 0.1f ? fv3(nl.z, 0.0f, -nl.x) : fv3(0.0f, -nl.z, nl.y);
   u = fnormalize(a);
   v = fcross(nl, u);
-  return fnormalize(fv3(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)),
-                        fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
-                        fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr))));
+  {
+    const fv r = fv3(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)), fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
+                     fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr)));
+    return unit ? fnormalize(r) : fnormalize2(r);
+  }
 }
 
 /* The hit point's plane distance n / d_a (:103, n = k - o_a) in the contract: one Markstein
@@ -838,6 +892,23 @@ static float c_hit_t(float n, float da, float t) {
  * quotient; the pdf only weights a sample, it places no geometry, and the correction cost the GPU
  * two VALU per loop iteration.) */
 static float c_div(float n, float d) { return n * spt_oracle_rcp_nr(d); }
+
+/* PDF_inverse * BRDF of :471-472 for a NEE shadow ray (x, d) whose nearest hit is the light at
+ * t. Unit directions: |area * d.y / t^2| * |d.nl / pi| as written. Free-scale (c_unit_dirs): d is
+ * light_vec itself; with dl = d/|d| and the distance t|d| the same quantity is
+ * (area/pi) |d.y| |d.nl| / (t^2 (d.d)^2), with no square root, rounded as written here. */
+static float c_nee_weight(const c_ctx* C, fv d, fv nl, float t) {
+  if (C->unit) {
+    const float pdf = fabsf(c_div(C->P->light_area * d.y, t * t));
+    const float brdf = fabsf(fdot(d, nl) * 0.318309886183790672f);
+    return pdf * brdf;
+  }
+  {
+    const float num = fabsf(d.y) * fabsf(fdot(d, nl));
+    const float vv = fdot(d, d);
+    return (num * C->nee_c) * spt_oracle_rcp_nr((t * t) * (vv * vv));
+  }
+}
 
 typedef struct {
   uint64_t samples, path_rays, shadow_rays, vertices, nee_events, nee_light_hits, cosine_samples,
@@ -871,9 +942,10 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
     const float su = (((float)px - 0.5f) + u16(r[0], r[1])) * inv_w;
     const float sv = (((float)(P->height - py - 1) - 0.5f) + u16(r[2], r[3])) * inv_h;
     o = fv3(cam[0], cam[1], cam[2]);
-    d = fnormalize(fv3(fmaf(cam[9], sv, fmaf(cam[6], su, cam[3])) - cam[0],
-                       fmaf(cam[10], sv, fmaf(cam[7], su, cam[4])) - cam[1],
-                       fmaf(cam[11], sv, fmaf(cam[8], su, cam[5])) - cam[2]));
+    d = fv3(fmaf(cam[9], sv, fmaf(cam[6], su, cam[3])) - cam[0],
+            fmaf(cam[10], sv, fmaf(cam[7], su, cam[4])) - cam[1],
+            fmaf(cam[11], sv, fmaf(cam[8], su, cam[5])) - cam[2]);
+    d = C->unit ? fnormalize(d) : fnormalize2(d);
   }
   st->samples++;
   for (;;) {
@@ -1012,7 +1084,8 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
           xl = fmaf(u01(r[0]), P->light_dx, P->light_x0);
           zl = fmaf(u01(r[1]), P->light_dz, P->light_z0);
         }
-        dl = fnormalize(fv3(xl - x.x, P->light_y - x.y, zl - x.z));
+        dl = fv3(xl - x.x, P->light_y - x.y, zl - x.z); /* light_vec :367 */
+        if (C->unit) dl = fnormalize(dl);              /* else free-scale (c_unit_dirs) */
         if (id == P->light_id || c_light_accepts(C, x, dl)) st->shadow_traced++;
         sh = c_intersect(C, x, dl, &ts, &ids);
         if (g_proof_on) {
@@ -1026,18 +1099,16 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         st->nee_events++;
         st->shadow_rays++;
         if (ids == P->light_id) {
-          const float pdf = fabsf(c_div(P->light_area * dl.y, ts * ts));
-          const float brdf = fabsf(fdot(dl, nl) * 0.318309886183790672f);
           st->nee_light_hits++;
-          w = pdf * brdf;
+          w = c_nee_weight(C, dl, nl, ts);
           dn = dl;
           carried = 1; c_hit = sh; c_t = ts; c_id = ids;
         } else {
-          dn = c_cosine(nl, r[2], r[3], (P->flags & SPT_FLAG_UNIFORM_SCATTER) != 0);
+          dn = c_cosine(nl, r[2], r[3], (P->flags & SPT_FLAG_UNIFORM_SCATTER) != 0, C->unit);
           st->cosine_samples++;
         }
       } else {
-        dn = c_cosine(nl, r[2], r[3], (P->flags & SPT_FLAG_UNIFORM_SCATTER) != 0);
+        dn = c_cosine(nl, r[2], r[3], (P->flags & SPT_FLAG_UNIFORM_SCATTER) != 0, C->unit);
         st->cosine_samples++;
       }
       L = fv3(fmaf(T.x, e.x, L.x), fmaf(T.y, e.y, L.y), fmaf(T.z, e.z, L.z));
@@ -1121,9 +1192,7 @@ int spt_oracle_counter_render(const spt_prim* prims, int n, const spt_camera* ca
   CP = (c_prim*)malloc(sizeof(c_prim) * (size_t)n);
   memset(&tot, 0, sizeof tot);
   c_prims_from_spt(prims, n, CP);
-  C.prims = CP; C.n = n; C.P = P; C.key[0] = SPT_PHILOX_KEY0; C.key[1] = SPT_PHILOX_KEY1;
-  C.n_tests = c_build_tests(CP, n, P->light_id, CT);
-  C.tests = CT;
+  c_ctx_init(&C, prims, CP, n, P, CT);
   for (i = 0; i < 3; i++) {
     camf[i] = (float)cam->origin[i];
     camf[3 + i] = (float)cam->lower_left_corner[i];
@@ -1195,9 +1264,7 @@ int spt_oracle_counter_render_pixels(const spt_prim* prims, int n, const spt_cam
   CP = (c_prim*)malloc(sizeof(c_prim) * (size_t)n);
   memset(&tot, 0, sizeof tot);
   c_prims_from_spt(prims, n, CP);
-  C.prims = CP; C.n = n; C.P = P; C.key[0] = SPT_PHILOX_KEY0; C.key[1] = SPT_PHILOX_KEY1;
-  C.n_tests = c_build_tests(CP, n, P->light_id, CT);
-  C.tests = CT;
+  c_ctx_init(&C, prims, CP, n, P, CT);
   for (i = 0; i < 3; i++) {
     camf[i] = (float)cam->origin[i];
     camf[3 + i] = (float)cam->lower_left_corner[i];

@@ -115,6 +115,19 @@ __device__ __forceinline__ float rsq_nr(float x) {
   return y;
 }
 
+// The same with two Newton steps (relative error < 5e-6): the free-scale contract's normalize
+// (oracle c_unit_dirs), where a path direction need only be unit to ~1e-4.
+__device__ __forceinline__ float rsq_nr2(float x) {
+  float y = __uint_as_float(0x5F375A86u - (__float_as_uint(x) >> 1));
+  const float h = 0.5f * x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float hy = h * y;
+    y = y * fmaf(-hy, y, 1.5f);
+  }
+  return y;
+}
+
 // Materialise v here, unconditionally: LLVM turns `c ? a : expensive(b)` back into a branch around
 // the expensive side, and each such branch costs exec-mask SALU, the loop's binding resource.
 template <typename T>
@@ -133,6 +146,13 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
   const float inv = rsq_nr(l2);
   return mk(v.x * inv, v.y * inv, v.z * inv);
 }
+// The free-scale contract's normalize (oracle fnormalize2): rsq with two Newton steps.
+__device__ __forceinline__ f3 normalize3_2(f3 v) {
+  const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+  const float inv = rsq_nr2(l2);
+  return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+__device__ __forceinline__ f3 normalize_dir(f3 v, bool unit) { return unit ? normalize3(v) : normalize3_2(v); }
 // operator% :56-58
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -187,21 +207,23 @@ __device__ __forceinline__ void disk_dir(uint32_t ra, float& c_out, float& s_out
 // axis-aligned (rect-only scenes); otherwise it is tested per lane, as the oracle does.
 // uniform: the reference's commented-out uniform hemisphere (:352-359), radial sqrt(r2(2-r2)) and
 // normal component 1-r2 (SPT_FLAG_UNIFORM_SCATTER; oracle c_cosine).
+// unit: the unit-direction contract (rsq_nr) or the free-scale one (rsq_nr2; oracle c_unit_dirs).
 template <bool AXIS = false>
-__device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool uniform = false) {
+__device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool uniform, bool unit) {
   const float xi2 = u01(rb);
   float s, c;
   disk_dir(ra, c, s);  // the azimuth r1 = 2*pi*xi1 of :343
   float r2s, s1;
   if (uniform) {
     const float m = xi2 * (2.0f - xi2);
-    r2s = m * rsq_nr(m);
+    r2s = m * (unit ? rsq_nr(m) : rsq_nr2(m));
     s1 = 1.0f - xi2;
   } else {
     // Contract (oracle c_cosine): sqrt(r2) and sqrt(1 - r2) of :343-347 scaled by 1/sqrt(1 - r2),
     // since the kernel normalizes the direction anyway: R = sqrt(r2 / (1 - r2)) with ONE rsqrt,
     // R = r2 * rsq(r2 * (1 - r2)) (r2 = 0 gives 0), and a normal component of exactly 1.
-    r2s = xi2 * rsq_nr(xi2 * (1.0f - xi2));
+    const float q = xi2 * (1.0f - xi2);
+    r2s = xi2 * (unit ? rsq_nr(q) : rsq_nr2(q));
     s1 = 1.0f;
   }
   const float cr = c * r2s, sr = s * r2s;
@@ -221,9 +243,7 @@ __device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool u
   return mk(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)), fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
             fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr)));
 }
-__device__ __forceinline__ f3 cosine_dir(f3 nl, uint32_t ra, uint32_t rb) {
-  return normalize3(cosine_vec(nl, ra, rb));
-}
+
 
 // 1.31 fixed-point per-sample contribution (order-independent, exact integer accumulation):
 // min(L/spp, 1) * 2^31 truncated (oracle c_fix). scale = inv_spp * 2^31 (exact), and

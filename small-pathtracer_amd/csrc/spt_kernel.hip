@@ -146,6 +146,8 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // Sphere NEE kernel: vertices above early_y0 (every sphere's top + 1) in the HEAD room resolve
   // their light-accepted shadow rays early (early_room_proven); +inf when the host cannot prove it
   float early_y0;
+  int unit_dirs;  // oracle c_unit_dirs: the scene has a sphere or a REFR primitive
+  float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
   unsigned long long* accum;  // [n_local_pix][3] 32.32 fixed point
   uint32_t* queue;            // [0] = next unit
   unsigned long long* stats;  // [8]
@@ -186,6 +188,10 @@ struct Topo {
   static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
   static constexpr bool WIDE = WIDE_;  // fp64 wide spheres may occur (their own kernel: VGPRs)
+  // Ray-direction contract (oracle c_unit_dirs): 1 = unit directions (spheres, REFR), 0 = free-scale
+  // (rect-only DIFF scenes: path directions normalised with rsq_nr2, the NEE vector not at all),
+  // -1 = KParams::unit_dirs at run time (the generic kernels)
+  static constexpr int DIRS = MAT_ ? -1 : (SPH_ ? 1 : 0);
 };
 // rect[] of :287-311 (light = XZ #3 -> pos 8); tests: 3 XY pairs, XZ floor/ceiling pair + light +
 // 2 box tops, 3 YZ pairs
@@ -195,6 +201,9 @@ using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 // Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
 // no SPEC/REFR stack and branch words, 8 waves/SIMD instead of the generic kernel's 6.
 using TopoSphDiff = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, false>;
+// Any other rect-only, all-DIFF, cosine-scatter scene (uploaded geometry, run-time loops): the
+// free-scale direction contract at compile time (Topo::DIRS 0), no sphere loop.
+using TopoRectDiff = Topo<-1, -1, -1, false, -1>;
 // Scenes with wide spheres (radius >= SPT_WIDE_SPHERE_RADIUS, tested in fp64: the classic smallpt
 // box): the generic kernel plus the fp64 sphere loop, kept apart because the doubles cost VGPRs.
 using TopoGenericWide = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, true, true>;
@@ -232,6 +241,16 @@ template <class CF> __device__ __forceinline__ int light_id_of(const SPT_CONST K
 }
 template <class CF> __device__ __forceinline__ int rr_depth_of(const SPT_CONST KParams* P) {
   if constexpr (CF::LREF == 1) return kRefRrDepth; else return P->rr_depth;
+}
+// The ray-direction contract of the launch (oracle c_unit_dirs; Topo::DIRS).
+template <class TP>
+__device__ __forceinline__ bool unit_dirs_of(const KParams* Pg) {
+  if constexpr (TP::DIRS >= 0) {
+    (void)Pg;
+    return TP::DIRS == 1;
+  } else {
+    return cptr(Pg)->unit_dirs != 0;
+  }
 }
 template <class TP>
 __device__ __forceinline__ auto rects_of(const SPT_CONST SceneGeo* G) {
@@ -577,6 +596,23 @@ __device__ __forceinline__ float hit_plane_t(float n, float da, float ia, float 
 // n / d of the contract where it only weights a sample (the NEE pdf; oracle c_div): n * rcp_nr(d).
 __device__ __forceinline__ float div_nr(float n, float d) { return n * rcp_nr(d); }
 
+// PDF_inverse * BRDF of :471-472 for a NEE shadow ray (x, d) whose nearest hit is the light at t
+// (oracle c_nee_weight). Unit directions: |area d.y / t^2| |d.nl / pi| as written. Free-scale: d is
+// light_vec (:367) itself, not normalised; with dl = d/|d| and the distance t|d| the same quantity
+// is (area/pi) |d.y| |d.nl| / (t^2 (d.d)^2): no square root, and the normalize of the shadow
+// direction (18 VALU per vertex) is gone.
+__device__ __forceinline__ float nee_weight(bool unit, f3 d, f3 nl, float t, float larea, float nee_c) {
+  if (unit) {
+    const float pdf = fabsf(div_nr(larea * d.y, t * t));            // :471
+    const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
+    return pdf * brdf;
+  }
+  const float num = fabsf(d.y) * fabsf(dot3(d, nl));
+  const float vv = dot3(d, d);
+  return (num * nee_c) * rcp_nr((t * t) * (vv * vv));
+}
+constexpr float kRefNeeC = (float)(1296.0 / 3.14159265358979323846);  // kRefLarea / pi
+
 __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
   return (uint32_t)(((uint64_t)n * m) >> sh);
 }
@@ -859,9 +895,10 @@ render_kernel(const KParams* __restrict__ Pg) {
     if (ls - kStCam < 3u) {
       const bool cam = ls == kStCam;
       if (ls != kStSpec) SPT_REGION(cam ? 3 : 8);
-      f3 v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
+      const bool unit = unit_dirs_of<TP>(Pg);
+      f3 v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0, unit);
       if (SPT_PROBE & 8) {
-        const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0);
+        const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0, unit);
         if (opq(0u) != 0u) v = v2;
       }
       // the vertex this ray leads to: depth + 1 (depth == 0 for a new sample's camera ray)
@@ -888,7 +925,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         }
         v = mk(cam ? vc.x : v.x, cam ? vc.y : v.y, cam ? vc.z : v.z);  // o: set at the path end
       }
-      const f3 dn = normalize3(v);
+      const f3 dn = normalize_dir(v, unit);  // rsq_nr2 in the free-scale contract
       if constexpr (TP::MAT) {  // a SPEC/REFR direction is set already
         const bool kd = ls == kStSpec;
         d = mk(kd ? d.x : dn.x, kd ? d.y : dn.y, kd ? d.z : dn.z);
@@ -930,9 +967,8 @@ render_kernel(const KParams* __restrict__ Pg) {
         l_hit += lh ? 1u : 0u;
         if constexpr (!TP::SPH) ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
-        const float pdf = fabsf(div_nr(larea * d.y, t * t));            // :471
-        const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
-        const float w = lh ? pdf * brdf : 1.0f;
+        const float nee_c = CF::LREF == 1 ? kRefNeeC : D->nee_c;
+        const float w = lh ? nee_weight(unit_dirs_of<TP>(Pg), d, nl, t, larea, nee_c) : 1.0f;
         T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
         // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
         // random draw; anything else is shaded with that vertex's own Philox words.
@@ -1103,7 +1139,9 @@ render_kernel(const KParams* __restrict__ Pg) {
               zl = fmaf(u01(r.y), D->ldz, D->lz0);
             }
             const float ly = CF::LREF == 1 ? kRefLy : D->ly;
-            const f3 dl = normalize3(mk(xl - x.x, ly - x.y, zl - x.z));
+            // light_vec (:367); normalised only in the unit-direction contract (nee_weight)
+            const f3 vl = mk(xl - x.x, ly - x.y, zl - x.z);
+            const f3 dl = unit_dirs_of<TP>(Pg) ? normalize3(vl) : vl;
             if constexpr (!kNeeByIdentity) l_nee += term ? 0u : 1u;
             const SPT_CONST SceneGeo* G2 = TP::CONSTGEO ? nullptr : cptr(D->geo);
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
@@ -1148,9 +1186,7 @@ render_kernel(const KParams* __restrict__ Pg) {
             l_early += ea ? 1u : 0u;
             ++l_shadow;
           }
-          const float pdf = fabsf(div_nr(kRefLarea * d.y, t * t));          // :471
-          const float brdf = fabsf(dot3(d, nl) * 0.318309886183790672f);  // :472
-          const float w = lh ? pdf * brdf : 1.0f;
+          const float w = lh ? nee_weight(unit_dirs_of<TP>(Pg), d, nl, t, kRefLarea, kRefNeeC) : 1.0f;
           T = mk(T.x * w, T.y * w, T.z * w);
           const DevPrim& H = s_prims[kRefLightId];
           const f3 Le = mk(fmaf(T.x, H.ex, L.x), fmaf(T.y, H.ey, L.y), fmaf(T.z, H.ez, L.z));
@@ -1312,12 +1348,13 @@ static spt_status fail(spt_status s, const std::string& msg) {
 // level).
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
-       KV_SPHDIFF_NEE, KV_COUNT };
+       KV_SPHDIFF_NEE, KV_RECTDIFF, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
     render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>,
-    render_kernel<TopoGenericWide, CfgRuntime>, render_kernel<TopoSphDiff, CfgSphNee>};
+    render_kernel<TopoGenericWide, CfgRuntime>, render_kernel<TopoSphDiff, CfgSphNee>,
+    render_kernel<TopoRectDiff, CfgRuntime>};
 
 struct spt_context {
   int device = 0;
@@ -1673,7 +1710,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   else if (cconst) kv = KV_CONST;
   else if (cornell) kv = KV_CORNELL;
   else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
-    kv = kcap >= 3 && K.light_black && lref && p->nee_prob >= 1.0f &&
+    kv = g.n_sph == 0 ? KV_RECTDIFF
+         : kcap >= 3 && K.light_black && lref && p->nee_prob >= 1.0f &&
                  p->light_mode == SPT_LIGHT_GLIBC_WRAP && light_pos >= 0 &&
                  prims[p->light_id].kind == SPT_RECT_XZ
              ? KV_SPHDIFF_NEE
@@ -1750,6 +1788,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
   K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
+  // Ray-direction contract (oracle c_unit_dirs): unit directions iff a sphere or a REFR primitive
+  K.unit_dirs = 0;
+  for (int i = 0; i < n_prims; ++i)
+    if (prims[i].kind == SPT_SPHERE || prims[i].refl == SPT_REFR) K.unit_dirs = 1;
+  K.nee_c = (float)((double)p->light_area / 3.14159265358979323846);
   c->n_prims = n_prims;
   c->last = K;
   c->samples = (uint64_t)K.n_local_pix * (uint64_t)p->spp;
