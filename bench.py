@@ -151,22 +151,33 @@ def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
 
 
 def reference_baseline(cfg, budget_s: float, threads: int = 1):
-    """The reference itself (oracle/_ref/smallpt_{nee,cos}: /root/reference/src/smallpt.cpp compiled
-    by oracle/build_ref.sh with the SURVEY Appendix A patch) on the same image size, with spp scaled
-    to a bounded sample of ~budget_s; None when the binary is absent (it is built only where the
-    reference is). threads == 1: the build as shipped (its OpenMP pragma :526 is commented out).
-    threads > 1: the reference's own OpenMP loop (smallpt_*_omp: pragma :526 enabled, row loop
-    :528 made canonical) on that many host cores."""
+    """The reference itself (oracle/_ref/smallpt_*: /root/reference/src/smallpt.cpp compiled by
+    oracle/build_ref.sh with the SURVEY Appendix A patch) with spp scaled to a bounded sample of
+    ~budget_s; None when the binary is absent (it is built only where the reference is).
+    threads == 1: the build as shipped (its OpenMP pragma :526 is commented out). threads > 1: the
+    reference's own OpenMP loop (smallpt_*_omp: pragma :526 enabled, row loop :528 made canonical)
+    on that many host cores (HEAD scene only).
+    C1-C4 (the HEAD scene): smallpt_nee / smallpt_cos. C5 (32 spheres, depth cap 16): smallpt_sph16,
+    the reference's own Sphere class (:223-254) in C5's scene with the cap. The 4096^2 configs run
+    the reference at 1024^2 (the same square camera, so the same distribution of pixel-sample work):
+    one 4096^2 pass of the reference is ~25 s (C4) or minutes (C5) plus a 200 MB P3 write."""
     import subprocess
     import tempfile
 
-    if cfg["scene"] != "cornell" or cfg["max_depth"] != 0:
+    if cfg["scene"] == "cornell" and cfg["max_depth"] == 0:
+        est = "nee" if cfg["nee_prob"] >= 1 else "cos"
+    elif cfg["scene"] == "spheres32" and cfg["max_depth"] == 16 and cfg["nee_prob"] >= 1:
+        if threads > 1:
+            return None
+        est = "sph16"
+    else:
         return None
-    est = "nee" if cfg["nee_prob"] >= 1 else "cos"
     binary = os.path.join(ROOT, "oracle", "_ref", f"smallpt_{est}" + ("_omp" if threads > 1 else ""))
     if not os.path.exists(binary):
         return None
     w, h = cfg["width"], cfg["height"]
+    if w * h > 1024 * 1024:
+        w, h = w * 1024 // max(w, h), h * 1024 // max(w, h)
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     with tempfile.TemporaryDirectory() as tmp:
         def run(spp):
@@ -186,8 +197,9 @@ def reference_baseline(cfg, budget_s: float, threads: int = 1):
     return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
             "host_cpus": os.cpu_count(), "kind": "reference",
             "sample": f"{w}x{h} @ {spp} spp = {w * h * spp} samples in {dt:.1f} s (whole image incl. "
-                      f"its P3 write); {os.path.relpath(binary, ROOT)} = the reference compiled from "
-                      f"its own sources, g++ -O3, {how}"}
+                      f"its P3 write{'' if (w, h) == (cfg['width'], cfg['height']) else ', at 1024^2: same camera aspect'}); "
+                      f"{os.path.relpath(binary, ROOT)} = the reference compiled from its own sources, "
+                      f"g++ -O3, {how}"}
 
 
 def image_writer(spt, full, w, h, with_cpu: bool):
@@ -258,14 +270,39 @@ def main() -> None:
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--kernel-level", default="auto", help="A/B only: cap the kernel specialisation "
                     "(auto | generic | cornell | const; spt_params.flags, never changes results)")
-    ap.add_argument("--verify-gather", action="store_true",
-                    help="rank 0 re-renders the whole image alone and checks the gathered one bit for bit")
+    ap.add_argument("--verify-gather", dest="verify_gather", action="store_true", default=None,
+                    help="rank 0 re-renders the whole image alone and checks the gathered one bit for "
+                         "bit (default on for N > 1: the RCCL gather has not run on hardware before)")
+    ap.add_argument("--no-verify-gather", dest="verify_gather", action="store_false")
+    ap.add_argument("--gather", choices=["spt", "torch"], default="spt",
+                    help="N > 1 over nccl: the library's gather (spt_comm: grouped ncclSend/ncclRecv "
+                         "+ de-interleave kernel) or torch.distributed.gather of the shards (RCCL) "
+                         "with the de-interleave as torch indexing on rank 0")
+    ap.add_argument("--init-timeout", type=float, default=300.0,
+                    help="seconds allowed for the RCCL / process-group set-up; past it the rank "
+                         "prints an error and exits with status 3 (no retry)")
     args = ap.parse_args()
+
+    import datetime
+    import threading
 
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.verify_gather is None:
+        args.verify_gather = world > 1
+
+    # Bounded set-up: a rank that cannot join the process group or the RCCL communicator (a peer
+    # missing, a wrong address) exits with a clear error instead of hanging the job.
+    def init_expired():
+        log(f"bench.py: rank {os.environ.get('RANK', '0')}: process-group / RCCL set-up did not "
+            f"finish within {args.init_timeout:.0f} s; exiting with status 3")
+        os._exit(3)
+    watchdog = threading.Timer(args.init_timeout, init_expired)
+    watchdog.daemon = True
+    if world > 1:
+        watchdog.start()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -276,10 +313,11 @@ def main() -> None:
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
+        tmo = datetime.timedelta(seconds=args.init_timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
 
     spt = importlib.import_module("small-pathtracer_amd")
     sd = importlib.import_module("small-pathtracer_amd.distributed")
@@ -306,7 +344,11 @@ def main() -> None:
     shard = torch.zeros((max_rows, w, 3), dtype=torch.float32, device="cuda")
     full = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
     comm = None
-    if world > 1 and backend == "nccl":
+    use_torch_gather = world > 1 and backend == "nccl" and args.gather == "torch"
+    # torch.distributed.gather into rank 0's pre-allocated slots, de-interleaved on the device
+    # (distributed.gather_rows, the path the gloo tests cover)
+    slots = [torch.zeros_like(shard) for _ in range(world)] if use_torch_gather and rank == 0 else None
+    if world > 1 and backend == "nccl" and not use_torch_gather:
         # the framebuffer gather of SURVEY §8e in the library (spt_comm: C++ over RCCL, grouped
         # ncclSend/ncclRecv to rank 0 + the de-interleave kernel); torch.distributed only carries
         # the RCCL unique id from rank 0 to the others
@@ -322,6 +364,8 @@ def main() -> None:
         if comm is not None:  # one RCCL gather to rank 0, on the render's stream
             comm.gather(params, shard.data_ptr(), full.data_ptr() if rank == 0 else 0,
                         stream.cuda_stream)
+        elif use_torch_gather:  # torch.distributed.gather over RCCL, de-interleave on rank 0
+            sd.gather_rows(shard, rows_of, full, gather_list=slots)
         elif world > 1:
             host = sd.gather_rows(shard.cpu(), rows_of, full.cpu() if rank == 0 else None)
             if rank == 0:
@@ -329,6 +373,7 @@ def main() -> None:
         else:
             full.copy_(shard[: len(my_rows)])
 
+    watchdog.cancel()  # set-up done (the first gather below has its own collective timeout)
     for _ in range(args.warmup):
         step()
     kstats.clear()
@@ -417,14 +462,17 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: the reference's Cornell-box scene (smallpt.cpp:287-311) and camera "
-                    "(:521), Philox4x32-10 stream seed 1",
+            "data": ("synthetic: the reference's Cornell-box scene (smallpt.cpp:287-311)"
+                     if cfg["scene"] == "cornell" else
+                     "synthetic: C5's 32-sphere scene (the room and light of smallpt.cpp:288-294 plus "
+                     "32 DIFF spheres of the reference's Sphere class :223-254)")
+                    + " and camera (:521), Philox4x32-10 stream seed 1",
             "config": {"workload": cfg["desc"] + (f", weak-scaled to {spp} spp over {world} GPUs"
                                                    if scaling == "weak" and world > 1 else ""),
                        "width": w, "height": h, "spp": spp,
                        "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",
                        "parallelism": (f"row-tile x{world} (tile 8 rows, cyclic) + one gather to rank 0 "
-                                       f"({'RCCL' if backend == 'nccl' else backend})")
+                                       f"({('RCCL, ' + ('torch.distributed.gather' if use_torch_gather else 'spt_comm grouped send/recv')) if backend == 'nccl' else backend})")
                                       if world > 1 else "1 GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),

@@ -110,8 +110,11 @@ typedef struct spt_params {
 enum { SPT_KERNEL_LEVEL_AUTO = 0, SPT_KERNEL_LEVEL_GENERIC = 1, SPT_KERNEL_LEVEL_CORNELL = 2,
        SPT_KERNEL_LEVEL_CONST = 3 };
 
-/* Philox4x32-10 key (fixed, so the key schedule is compile-time) and counter layout:
- * ctr = (pixel = y*w + x, sample, vertex | stream << 31, seed). */
+/* The counter RNG: Philox4x32 with SPT_PHILOX_ROUNDS rounds (7: the Random123 paper's smallest
+ * Crush-resistant count for Philox4x32; its library default is 10), a fixed key (so the key
+ * schedule is compile-time) and the counter ctr = (pixel = y*w + x, sample, vertex | stream << 31,
+ * seed). */
+#define SPT_PHILOX_ROUNDS 7
 #define SPT_PHILOX_KEY0 0x53505430u /* "SPT0" */
 #define SPT_PHILOX_KEY1 0x53505431u /* "SPT1" */
 

@@ -428,11 +428,16 @@ double spt_oracle_prim_intersect(const spt_prim* s, const double o[3], const dou
 #define PH_M1 0xCD9E8D57u
 #define PH_W0 0x9E3779B9u
 #define PH_W1 0xBB67AE85u
-void spt_oracle_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+/* Philox4x32 with R rounds (Salmon et al. SC'11, the Random123 round function). R = 10 is
+ * Random123's default (checked against its known-answer vectors); the counter-mode contract uses
+ * R = SPT_PHILOX_ROUNDS = 7, the paper's smallest Crush-resistant round count for Philox4x32
+ * (round 3: three rounds fewer per vertex are 18 VALU issue slots, -3.5 % kernel time at C3). */
+void spt_oracle_philox_r(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4],
+                         int rounds) {
   uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
   uint32_t k0 = key_in[0], k1 = key_in[1];
   int r;
-  for (r = 0; r < 10; r++) {
+  for (r = 0; r < rounds; r++) {
     const uint64_t p0 = (uint64_t)PH_M0 * c0, p1 = (uint64_t)PH_M1 * c2;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
@@ -444,6 +449,13 @@ void spt_oracle_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint3
     k1 += PH_W1;
   }
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+void spt_oracle_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  spt_oracle_philox_r(ctr_in, key_in, out, 10);
+}
+/* The contract's generator (c_path): Philox4x32-SPT_PHILOX_ROUNDS. */
+static void c_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  spt_oracle_philox_r(ctr_in, key_in, out, SPT_PHILOX_ROUNDS);
 }
 
 typedef struct { float x, y, z; } fv;
@@ -543,16 +555,25 @@ void spt_oracle_sincos2pi(float xi, float* s_out, float* c_out) {
  * = theta in [0, pi/4) (21 bits; theta = u * (pi/2) * 2^-22, the sincos2pi polynomials in quarter
  * turns r = u * 2^-22 < 1/2). Uniform on the circle like 2*pi*xi (8 octants x 2^21 angles), without
  * the quarter-turn reduction or a quadrant rotation. */
+/* The azimuth polynomials (contract, round 3): minimax fits on theta in [0, pi/4] (r in [0, 1/2]
+ * quarter turns) with one term fewer than the Taylor sums above -- sin r(s1 + s3 r^2 + s5 r^4 +
+ * s7 r^6), cos 1 + r^2(c2 + c4 r^2 + c6 r^4) -- whose fp32 evaluation is within 1.3e-7 relative of
+ * sin/cos (the 5-term Taylor forms: 1.6e-7 / 1.2e-7), two fma fewer per cosine sample. */
+#define DD_S1 1.5707963705062866f
+#define DD_S3 -0.6459634900093079f
+#define DD_S5 0.07968003302812576f
+#define DD_S7 -0.004601659253239632f
+#define DD_C2 -1.2336976528167725f
+#define DD_C4 0.2536032199859619f
+#define DD_C6 -0.020417289808392525f
 void spt_oracle_disk_dir(uint32_t ra, float* c_out, float* s_out) {
   const float r = (float)((ra >> 8) & 0x1FFFFFu) * 0x1p-22f;
   const float r2 = r * r;
-  float ps = fmaf(r2, SC_S9, SC_S7), pc = fmaf(r2, SC_C8, SC_C6), sn, cs, t;
-  ps = fmaf(r2, ps, SC_S5);
-  ps = fmaf(r2, ps, SC_S3);
-  ps = fmaf(r2, ps, SC_S1);
+  float ps = fmaf(r2, DD_S7, DD_S5), pc = fmaf(r2, DD_C6, DD_C4), sn, cs, t;
+  ps = fmaf(r2, ps, DD_S3);
+  ps = fmaf(r2, ps, DD_S1);
   sn = r * ps;
-  pc = fmaf(r2, pc, SC_C4);
-  pc = fmaf(r2, pc, SC_C2);
+  pc = fmaf(r2, pc, DD_C2);
   cs = fmaf(r2, pc, 1.0f);
   if (ra & 0x20000000u) { t = cs; cs = sn; sn = t; }
   *c_out = asf(asu(cs) ^ (ra & 0x80000000u));
@@ -936,7 +957,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
   /* Camera ray :533-536. The jitter comes from the low bytes of vertex 1's Philox call (16 bits
    * each), so a sample start costs no extra RNG call; 1/w, 1/h are rounded once. */
   ctr[0] = pix; ctr[1] = s; ctr[2] = 1; ctr[3] = P->seed;
-  spt_oracle_philox(ctr, C->key, r);
+  c_philox(ctr, C->key, r);
   {
     const float inv_w = 1.0f / (float)P->width, inv_h = 1.0f / (float)P->height;
     const float su = (((float)px - 0.5f) + u16(r[0], r[1])) * inv_w;
@@ -993,11 +1014,11 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
      * vertex 1, whose low bytes were the camera jitter: its RR / NEE-mix draws (only needed when
      * rr_depth < 1 or 0 < nee_prob < 1) come from stream 1. */
     ctr[0] = pix; ctr[1] = s; ctr[2] = (uint32_t)depth | (branch << 24); ctr[3] = P->seed;
-    spt_oracle_philox(ctr, C->key, r);
+    c_philox(ctr, C->key, r);
     rl[0] = r[0]; rl[1] = r[1]; rl[2] = r[2]; rl[3] = r[3];
     if (depth == 1) {
       ctr[2] = 1u | 0x80000000u; /* stream 1 */
-      spt_oracle_philox(ctr, C->key, rl);
+      c_philox(ctr, C->key, rl);
     }
     {
       const float p = H->pmax;

@@ -18,19 +18,16 @@
 
 namespace spt {
 
-// ---- Philox4x32-10 (Salmon et al. SC'11), replaces erand48/rand() (utilities.h:26-51,
-// smallpt.cpp:365-366,460,533-534). Fixed key (SPT_PHILOX_KEY0/1): the whole key schedule is
-// compile-time, so each round is two v_mad_u64_u32 and four v_xor_b32 with literal/VGPR operands
-// and no SALU. Counter = (pixel, sample, vertex | stream << 31, seed).
+// ---- Philox4x32-R (Salmon et al. SC'11; R = SPT_PHILOX_ROUNDS = 7, include/spt.h), replaces
+// erand48/rand() (utilities.h:26-51, smallpt.cpp:365-366,460,533-534). Fixed key
+// (SPT_PHILOX_KEY0/1): the whole key schedule is compile-time, so each round is two
+// v_mad_u64_u32 and two xors. Counter = (pixel, sample, vertex | stream << 31, seed).
 constexpr uint32_t kPhM0 = 0xD2511F53u, kPhM1 = 0xCD9E8D57u;
 constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
 
 struct u4 { uint32_t x, y, z, w; };
 
-#ifndef SPT_PHILOX_ROUNDS
-#define SPT_PHILOX_ROUNDS 10  // A/B timing builds only: the contract (and the oracle) is 10 rounds
-#endif
-__device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+__device__ __forceinline__ u4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
   uint32_t k0 = SPT_PHILOX_KEY0, k1 = SPT_PHILOX_KEY1;
 #pragma unroll
   for (int r = 0; r < SPT_PHILOX_ROUNDS; ++r) {
@@ -47,28 +44,46 @@ __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
 // The same generator with the counter word c0 (the pixel) and c3 (the seed) fixed for a whole work
 // unit: round 1's product M0 * c0 and its xor with c3 and the first key word are computed once per
 // unit (PxKey), so each call saves one v_mad_u64_u32 and one v_xor. Bit-identical to
-// philox4x32_10(pix, c1, c2, seed).
-struct PxKey { uint32_t hi, lo; };  // hi(M0*pix) ^ seed ^ k1, lo(M0*pix)
+// philox4x32(pix, c1, c2, seed).
+// Round 2 multiplies that same word (round 1's n2, per unit) by M1, so its product is per unit too:
+// PxKey keeps hi(M1 * n2) ^ k0(round 2), lo(M1 * n2) and round 1's c3 = lo(M0 * pix), which saves a
+// second v_mad_u64_u32 per call.
+struct PxKey { uint32_t qhi, qlo, lo; };
 __device__ __forceinline__ PxKey philox_pixel_key(uint32_t pix, uint32_t seed) {
   const uint64_t p0 = (uint64_t)kPhM0 * pix;
-  return PxKey{(uint32_t)(p0 >> 32) ^ seed ^ (uint32_t)SPT_PHILOX_KEY1, (uint32_t)p0};
+  const uint32_t n2 = (uint32_t)(p0 >> 32) ^ seed ^ (uint32_t)SPT_PHILOX_KEY1;
+  const uint64_t q1 = (uint64_t)kPhM1 * n2;
+  return PxKey{(uint32_t)(q1 >> 32) ^ (uint32_t)(SPT_PHILOX_KEY0 + kPhW0), (uint32_t)q1, (uint32_t)p0};
 }
 // a ^ b ^ k in ONE full-rate v_bitop3_b32 (tools/valu_rates: v_xor and v_bitop3 issue at the same
 // rate), k a compile-time round key held in an SGPR: halves the xor count of a Philox round.
 __device__ __forceinline__ uint32_t xor3k(uint32_t a, uint32_t b, uint32_t k) {
   uint32_t r;
+#ifdef SPT_XOR_LIT  // A/B: two VOP2 xors, the key as a literal (no s_mov of the key into an SGPR)
+  asm("v_xor_b32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  asm("v_xor_b32_e32 %0, %1, %2" : "=v"(r) : "i"((int)k), "v"(r));
+#else
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+#endif
   return r;
 }
 __device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
   uint32_t k0 = SPT_PHILOX_KEY0, k1 = SPT_PHILOX_KEY1;
+  // round 1: the pixel word's product is per unit (philox_pixel_key)
   const uint64_t p1 = (uint64_t)kPhM1 * c2;
   uint32_t c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, c3 = pk.lo;
   c1 = (uint32_t)p1;
-  c2 = pk.hi;
   k0 += kPhW0; k1 += kPhW1;
+  // round 2: M1 * c2 is per unit as well (pk.qhi already holds its high word ^ k0)
+  {
+    const uint64_t p0 = (uint64_t)kPhM0 * c0;
+    const uint32_t n0 = pk.qhi ^ c1;
+    const uint32_t n2 = xor3k((uint32_t)(p0 >> 32), c3, k1);
+    c0 = n0; c1 = pk.qlo; c2 = n2; c3 = (uint32_t)p0;
+    k0 += kPhW0; k1 += kPhW1;
+  }
 #pragma unroll
-  for (int r = 1; r < SPT_PHILOX_ROUNDS; ++r) {
+  for (int r = 2; r < SPT_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)kPhM0 * c0;
     const uint64_t q1 = (uint64_t)kPhM1 * c2;
 #ifdef SPT_PHILOX_XOR2
@@ -185,16 +200,18 @@ __device__ __forceinline__ void sincos2pi(float xi, float& s_out, float& c_out) 
 // [0, pi/4) as quarter turns r = u * 2^-22 for the sincos2pi polynomials. No range reduction and no
 // quadrant rotation: two sign-bit inserts and one conditional swap.
 __device__ __forceinline__ void disk_dir(uint32_t ra, float& c_out, float& s_out) {
-  const float r = (float)__builtin_amdgcn_ubfe(ra, 8, 21) * 0x1p-22f;
+  // r = u * 2^-22 for the 21-bit u = bits 28..8: the float with bits 0x4B000000 | u is 2^23 + u,
+  // so fma(2^23 + u, 2^-22, -2) is u * 2^-22 exactly (the bits of (float)u * 0x1p-22f, with a
+  // full-rate v_or instead of a half-rate conversion and a multiply)
+  const float r = fmaf(__uint_as_float(__builtin_amdgcn_ubfe(ra, 8, 21) | 0x4B000000u), 0x1p-22f, -2.0f);
   const float r2 = r * r;
-  float ps = fmaf(r2, 0.000160441184787359821f, -0.00468175413531868810f);
-  float pc = fmaf(r2, 0.000919260274839426030f, -0.0208634807633529609f);
-  ps = fmaf(r2, ps, 0.0796926262461670451f);
-  ps = fmaf(r2, ps, -0.645964097506246254f);
-  ps = fmaf(r2, ps, 1.57079632679489662f);
+  // minimax sin / cos on [0, pi/4], 4 terms each (oracle DD_*: within 1.3e-7 relative in fp32)
+  float ps = fmaf(r2, -0.004601659253239632f, 0.07968003302812576f);
+  float pc = fmaf(r2, -0.020417289808392525f, 0.2536032199859619f);
+  ps = fmaf(r2, ps, -0.6459634900093079f);
+  ps = fmaf(r2, ps, 1.5707963705062866f);
   const float sn = r * ps;
-  pc = fmaf(r2, pc, 0.253669507901048014f);
-  pc = fmaf(r2, pc, -1.23370055013616983f);
+  pc = fmaf(r2, pc, -1.2336976528167725f);
   const float cs = fmaf(r2, pc, 1.0f);
   const bool sw = (ra & 0x20000000u) != 0u;
   const float c = sw ? sn : cs, s = sw ? cs : sn;

@@ -42,7 +42,10 @@ constexpr int kBlock = 256;
 // atomics), 128/256 slower for C3 (16.7/17.3 vs 16.0 ms: work hoarded in one wave's pool when the
 // queue drains) though faster for C2 (4.45 ms); a guided scheme (static first slice per wave, then
 // shares of what is left, 16..256) was 6 % slower on C3-C5.
-constexpr uint32_t kGrab = 64;
+#ifndef SPT_GRAB
+#define SPT_GRAB 64
+#endif
+constexpr uint32_t kGrab = SPT_GRAB;
 constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the queue atomics)
 // Launches with fewer lane-iterations per resident lane than SPT_SMALL_ITERS deal their units
 // almost all at once (SPT_SMALL_UNITS per lane) and balance by stealing (host, spt_render_async).
@@ -51,6 +54,9 @@ constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the 
 #endif
 #ifndef SPT_SMALL_UNITS
 #define SPT_SMALL_UNITS 1.5
+#endif
+#ifndef SPT_STEAL_MIN
+#define SPT_STEAL_MIN 1  // unstarted samples a donor must hold (in-wave stealing)
 #endif
 #ifdef SPT_WAVE_TIMES
 constexpr int kStatWords = 32 + 3 * 32768;  // diagnostic: per-wave start, end, iterations
@@ -613,6 +619,14 @@ __device__ __forceinline__ float nee_weight(bool unit, f3 d, f3 nl, float t, flo
 }
 constexpr float kRefNeeC = (float)(1296.0 / 3.14159265358979323846);  // kRefLarea / pi
 
+// The jittered raster coordinate (x - 0.5) + u * 2^-16 of :533 (u the 16-bit jitter draw) with
+// f128 = (x - 0.5) - 128: the float with bits 0x4B000000 | u is 2^23 + u exactly, and
+// fma(2^23 + u, 2^-16, f128) rounds the exact sum (x - 0.5) + u * 2^-16 once -- the same bits as
+// fmaf((float)u, 0x1p-16f, x - 0.5f), with a full-rate v_or instead of a half-rate conversion.
+__device__ __forceinline__ float jitter_fma(uint32_t lo, uint32_t hi, float f128) {
+  return fmaf(__uint_as_float(u16i(lo, hi) | 0x4B000000u), 0x1p-16f, f128);
+}
+
 __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
   return (uint32_t)(((uint64_t)n * m) >> sh);
 }
@@ -627,8 +641,9 @@ __device__ __forceinline__ void pixel_terms(const SPT_CONST KParams* Q, uint32_t
   const uint32_t tile = div_magic(lr, Q->m_tile, Q->sh_tile), within = lr - tile * T_;
   const int py = (int)((tile * (uint32_t)Q->shard_count + (uint32_t)Q->shard_index) * T_ + within);
   pk = philox_pixel_key((uint32_t)py * w + (uint32_t)px, Q->seed);
-  fx = (float)px - 0.5f;
-  fy = (float)(Q->height - py - 1) - 0.5f;
+  // camera raster terms (x - 0.5), (h - y - 1 - 0.5) of :533-534, less 128 (jitter_fma)
+  fx = ((float)px - 0.5f) - 128.0f;
+  fy = ((float)(Q->height - py - 1) - 0.5f) - 128.0f;
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -672,9 +687,10 @@ template <class TP, class CF>
 #define SPT_NUM_SGPR 80
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(SPT_NUM_SGPR)))
-// The sphere kernels allocate for 8 waves/SIMD explicitly: the NEE-specialised one otherwise takes
-// 65 VGPRs (7 waves); with the hint it fits 64 with no spills (the others are unaffected)
-__attribute__((amdgpu_waves_per_eu(TP::SPH && !TP::MAT && !TP::WIDE ? 8 : 1)))
+// The sphere kernels and the estimator-specialised HEAD kernels allocate for 8 waves/SIMD
+// explicitly: the sphere NEE kernel otherwise takes 65 VGPRs (7 waves), the HEAD NEE kernel 65 with
+// the round-2 Philox key (philox_pixel_key); with the hint both fit 64 with no spills
+__attribute__((amdgpu_waves_per_eu((TP::SPH && !TP::MAT && !TP::WIDE) || (TP::CONSTGEO && CF::NEE >= 0) ? 8 : 1)))
 render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
@@ -726,9 +742,9 @@ render_kernel(const KParams* __restrict__ Pg) {
   uint32_t branch = 0;    // path-tree position of a REFR split (counter word 2 bits 24+; MAT only)
   int sp = 0;             // pending refraction children in s_stack (MAT only)
   uint32_t lp = 0, s = 0, s_end = 0;
-  PxKey pk = PxKey{0, 0};  // Philox round-1 terms of the unit's pixel (philox_pixel_key)
+  PxKey pk = PxKey{0, 0, 0};  // Philox round-1/2 terms of the unit's pixel (philox_pixel_key)
   int depth = 0, vid = 0;  // depth: vertices of the current path so far (0 until its first)
-  float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5), (h - y - 1 - 0.5) of :533-534
+  float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5) - 128, (h - y - 1 - 0.5) - 128
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
   // o starts at the camera (the first ray of every sample is a camera ray; the path end resets it)
   f3 o = mk(cptr(Pg)->cam[0], cptr(Pg)->cam[1], cptr(Pg)->cam[2]);
@@ -857,7 +873,10 @@ render_kernel(const KParams* __restrict__ Pg) {
       uint64_t idle = __ballot(ls == kStIdle);
       if (idle != 0) {
         const uint32_t cur = s + (ls == kStCam ? 0u : 1u);  // first unstarted sample
-        uint64_t dm = __ballot(ls != kStIdle && s_end > cur + (ls == kStCam ? 1u : 0u));
+        // donors: lanes with more unstarted samples than the one they start next, and at least
+        // SPT_STEAL_MIN of them (every stolen range flushes its own sums: memory-side atomics)
+        uint64_t dm = __ballot(ls != kStIdle && s_end > cur + (ls == kStCam ? 1u : 0u) &&
+                               s_end >= cur + (uint32_t)SPT_STEAL_MIN);
         while (idle != 0 && dm != 0) {
           const int il = __builtin_ctzll(idle), dl = __builtin_ctzll(dm);
           idle &= idle - 1;
@@ -866,7 +885,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           const uint32_t dend = (uint32_t)__builtin_amdgcn_readlane((int)s_end, dl);
           const uint32_t mid = dcur + (dend - dcur) / 2u;  // donor keeps [.., mid), taker [mid, dend)
           const uint32_t d_lp = (uint32_t)__builtin_amdgcn_readlane((int)lp, dl);
-          const uint32_t d_hi = (uint32_t)__builtin_amdgcn_readlane((int)pk.hi, dl);
+          const uint32_t d_qhi = (uint32_t)__builtin_amdgcn_readlane((int)pk.qhi, dl);
+          const uint32_t d_qlo = (uint32_t)__builtin_amdgcn_readlane((int)pk.qlo, dl);
           const uint32_t d_lo = (uint32_t)__builtin_amdgcn_readlane((int)pk.lo, dl);
           const float d_fx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fx), dl));
           const float d_fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy), dl));
@@ -874,7 +894,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           s_end = tk ? dend : (lane == (uint32_t)dl ? mid : s_end);
           s = tk ? mid : s;
           lp = tk ? d_lp : lp;
-          pk.hi = tk ? d_hi : pk.hi;
+          pk.qhi = tk ? d_qhi : pk.qhi;
+          pk.qlo = tk ? d_qlo : pk.qlo;
           pk.lo = tk ? d_lo : pk.lo;
           fx = tk ? d_fx : fx;
           fy = tk ? d_fy : fy;
@@ -905,20 +926,19 @@ render_kernel(const KParams* __restrict__ Pg) {
       const uint32_t ctr2 = ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u);
       r = philox_px(pk, s, ctr2);
       if (SPT_PROBE & 1) {
-        const u4 r2 = philox_px(PxKey{opq(pk.hi), pk.lo}, s, ctr2);
+        const u4 r2 = philox_px(PxKey{opq(pk.qhi), pk.qlo, pk.lo}, s, ctr2);
         if (opq(0u) != 0u) r = r2;
       }
       {
         const SPT_CONST KParams* C = cptr(Pg);
         f3 vc;
         if constexpr (CF::CAMAX == 1) {  // fma(+-0, s, a) == a for a != 0; a == +-0 only meets - o
-          // fx + u * 2^-16 in one fma (the product is exact: the same single rounding as the add)
-          const float su = fmaf((float)u16i(r.x, r.y), 0x1p-16f, fx) * ck.iw;
-          const float sv = fmaf((float)u16i(r.z, r.w), 0x1p-16f, fy) * ck.ih;
+          const float su = jitter_fma(r.x, r.y, fx) * ck.iw;
+          const float sv = jitter_fma(r.z, r.w, fy) * ck.ih;
           vc = mk(fmaf(ck.h0, su, ck.l0) - ck.o0, fmaf(ck.v1, sv, ck.l1) - ck.o1, ck.l2 - ck.o2);
         } else {
-          const float su = fmaf((float)u16i(r.x, r.y), 0x1p-16f, fx) * C->inv_w;
-          const float sv = fmaf((float)u16i(r.z, r.w), 0x1p-16f, fy) * C->inv_h;
+          const float su = jitter_fma(r.x, r.y, fx) * C->inv_w;
+          const float sv = jitter_fma(r.z, r.w, fy) * C->inv_h;
           vc = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
                   fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
                   fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
@@ -1186,7 +1206,9 @@ render_kernel(const KParams* __restrict__ Pg) {
             l_early += ea ? 1u : 0u;
             ++l_shadow;
           }
-          const float w = lh ? nee_weight(unit_dirs_of<TP>(Pg), d, nl, t, kRefLarea, kRefNeeC) : 1.0f;
+          // (computed for every resolving lane: a branch around it cost exec-mask SALU)
+          const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, t, kRefLarea, kRefNeeC));
+          const float w = lh ? wl : 1.0f;
           T = mk(T.x * w, T.y * w, T.z * w);
           const DevPrim& H = s_prims[kRefLightId];
           const f3 Le = mk(fmaf(T.x, H.ex, L.x), fmaf(T.y, H.ey, L.y), fmaf(T.z, H.ez, L.z));
@@ -1406,6 +1428,10 @@ static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* c
   for (int i = 0; i < n; ++i) {
     if (prims[i].kind < SPT_RECT_XY || prims[i].kind > SPT_SPHERE)
       return fail(SPT_ERR_INVALID_ARG, "bad primitive kind");
+    // Sphere::normal (:248) is (x - p).norm(); the contract's (x - p) * (1/r) equals it only for
+    // r > 0 (a negative radius would flip the geometric normal of the REFR test :485)
+    if (prims[i].kind == SPT_SPHERE && !(prims[i].geom[0] > 0.0 && std::isfinite(prims[i].geom[0])))
+      return fail(SPT_ERR_INVALID_ARG, "sphere radius must be positive and finite");
     if (prims[i].refl < SPT_DIFF || prims[i].refl > SPT_REFR)
       return fail(SPT_ERR_INVALID_ARG, "bad material");
   }
@@ -1727,9 +1753,17 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
     double top = -INFINITY;
     for (int i = 7; ok && i < n_prims; ++i) {
-      ok = prims[i].kind == SPT_SPHERE && std::isfinite(prims[i].geom[0]) &&
-           std::isfinite(prims[i].geom[2]);
-      top = std::max(top, prims[i].geom[2] + std::fabs(prims[i].geom[0]));
+      const double* g = prims[i].geom;
+      ok = prims[i].kind == SPT_SPHERE && std::isfinite(g[0]) && std::isfinite(g[1]) &&
+           std::isfinite(g[2]) && std::isfinite(g[3]);
+      top = std::max(top, g[2] + std::fabs(g[0]));
+      // the fp32 rounding argument of early_room_proven holds for |op| < 200 (and r < 200): every
+      // sphere centre within 190 of every room corner, so no vertex in the room is farther away
+      for (int c = 0; ok && c < 8; ++c) {
+        const double cx = (c & 1) ? 99.0 : 1.0, cy = (c & 2) ? 81.6 : 0.0, cz = (c & 4) ? 170.0 : 0.0;
+        ok = std::sqrt((g[1] - cx) * (g[1] - cx) + (g[2] - cy) * (g[2] - cy) +
+                       (g[3] - cz) * (g[3] - cz)) < 190.0 && std::fabs(g[0]) < 190.0;
+      }
     }
     if (ok && top + 1.0 < 81.0) {
       float y0 = (float)(top + 1.0);
@@ -1767,7 +1801,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     const uint32_t waves = (uint32_t)(c->n_cu * c->bpc[kv] * (kBlock / 64));
     uint32_t sh = 1;  // 2^sh >= 2 x waves
     while ((1u << sh) < 2u * waves && sh < 31) ++sh;
+#ifdef SPT_GUIDED_ALWAYS  // A/B builds only
+    K.sh_guided = sh;
+#else
     K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
+#endif
   }
   K.chunk = chunk;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;

@@ -97,6 +97,18 @@ def test_invalid_arguments_fail_loudly(spt):
     assert e.value.status == 1
 
 
+@pytest.mark.parametrize("rad", [0.0, -6.0, float("inf"), float("nan")])
+def test_sphere_radius_must_be_positive(spt, rad):
+    """Sphere::normal (:248) is (x - p).norm(); the contract's (x - p) * (1/r) equals it only for
+    r > 0 (a negative radius would flip the geometric normal of the REFR test :485)."""
+    cam = spt.Camera(aspect=1.0)
+    scene = spt.spheres32_scene()
+    scene[9].geom[0] = rad
+    with pytest.raises(spt.SptError) as e:
+        spt.render(scene, cam, spt.default_params(width=8, height=8, spp=1))
+    assert e.value.status == 1 and "radius" in spt.load_library().spt_last_error().decode()
+
+
 def test_nee_needs_an_emitting_light(spt):
     """NEE (nee_prob > 0) weights shadow rays reaching prims[light_id] as light hits: a light id
     that is absent or does not emit is rejected (the classic box's HEAD id 6 is a ball there)."""

@@ -268,6 +268,52 @@ def test_early_nee_resolve_spheres_matches_oracle_proof(spt, oracle):
     assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
 
 
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_early_nee_resolve_random_low_spheres(spt, oracle, seed):
+    """Randomised sphere-only, all-DIFF scenes in the HEAD room (:287-294) whose spheres all lie
+    below y = 80 -- radii up to 99, centres below the floor and outside the room included: the host
+    enables the sphere kernel's early resolve above y0 = max top + 1 only when every centre is within
+    190 of every room corner (the fp32 rounding argument of early_room_proven). Enabled: the kernel's
+    count equals the oracle's claims, none contradicted by its own intersect; disabled: nothing is
+    resolved early. Image and statistics bit-exact either way."""
+    rng = np.random.default_rng(seed)
+    prims = list(spt.cornell_scene())[:7]
+    tops, near = [], True
+    corners = [(cx, cy, cz) for cx in (1.0, 99.0) for cy in (0.0, 81.6) for cz in (0.0, 170.0)]
+    for _ in range(int(rng.integers(1, 7))):
+        big = rng.random() < 0.4
+        r = float(rng.uniform(20, 99) if big else rng.uniform(1, 12))
+        yc = float(rng.uniform(-r - 5, 79 - r))
+        xc = float(rng.uniform(-80, 180) if big else rng.uniform(1 + r, 99 - r))
+        zc = float(rng.uniform(-80, 250) if big else rng.uniform(r, 170 - r))
+        p = spt.spt_prim()
+        p.kind = spt.SPHERE
+        p.geom[:] = [r, xc, yc, zc, 0.0]
+        p.c[:] = [float(v) for v in rng.uniform(0.1, 0.95, 3)]
+        prims.append(p)
+        tops.append(yc + r)
+        near = near and all(np.sqrt((xc - a) ** 2 + (yc - b) ** 2 + (zc - c) ** 2) < 190.0
+                            for a, b, c in corners)
+    y0 = np.float32(max(tops) + 1.0)
+    if float(y0) < max(tops) + 1.0:
+        y0 = np.nextafter(y0, np.float32(np.inf))
+    params = spt.default_params(width=96, height=72, spp=8, seed=seed, max_depth=12)
+    oracle.proof_check(True, sphere_y0=float(y0))
+    try:
+        gpu, gst, cpu, cst = _render_both(spt, oracle, prims, params)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    _assert_exact(gpu, cpu)
+    for k in spt.STAT_KEYS:
+        assert gst[k] == cst[k], k
+    if near:
+        assert bad == 0 and claims > 0, (claims, bad)
+        assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
+    else:
+        assert gst["shadow_proven"] == 0
+
+
 def test_c4_geometry_pixel_indices_beyond_2p24(spt, oracle):
     """4096x4096 (configs[3] image size) at 1 spp: pixel counters above 2^24 still match."""
     w = h = 4096

@@ -64,3 +64,24 @@ def test_shard_row_lists_partition():
     for h, t, n in [(768, 8, 8), (100, 8, 3), (5, 8, 4)]:
         rows = sd.shard_row_lists(h, t, n)
         assert sorted(np.concatenate(rows).tolist()) == list(range(h))
+
+
+def test_shard_zero_is_the_largest_shard(spt):
+    """spt_multi.hip sizes rank 0's receive slots (and bench.py its padded shard buffers) by shard 0:
+    with cyclic tiles (tile t -> rank t mod n) shard 0 never owns fewer rows than any other shard,
+    ragged last tiles and ranks without rows included (checked through the C ABI spt_shard_rows)."""
+    sd = importlib.import_module("small-pathtracer_amd.distributed")
+    cases = 0
+    for h in list(range(1, 70)) + [767, 768, 769, 1000, 4095, 4096, 4097]:
+        for t in (1, 2, 3, 7, 8, 16):
+            for n in (1, 2, 3, 5, 7, 8, 16):
+                counts = []
+                for k in range(n):
+                    p = spt.default_params(width=3, height=h, spp=1, tile_rows=t, shard_index=k,
+                                           shard_count=n)
+                    counts.append(len(spt.shard_rows(p)))
+                assert counts[0] == max(counts), (h, t, n, counts)
+                assert sum(counts) == h
+                assert sd.max_rows(sd.shard_row_lists(h, t, n)) == counts[0]
+                cases += 1
+    assert cases > 3000

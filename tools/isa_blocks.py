@@ -7,6 +7,23 @@ import re
 import sys
 
 
+# Issue cost in VALU slots (one slot = a full-rate wave64 instruction, 2 cycles on a SIMD-32),
+# measured by tools/valu_rates.hip (profiles/r01_valu_rates.txt): half-rate ops 2, transcendental 4.
+HALF = ("v_mad_u64_u32", "v_mad_i64_i32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_u32_u24",
+        "v_mul_hi_u32_u24", "v_mad_u32_u24", "v_cvt_", "v_perm_b32", "v_bfe_", "v_bfi_b32",
+        "v_add3_u32", "v_lshl_add_u32", "v_lshl_or_b32", "v_and_or_b32", "v_or3_b32", "v_med3_",
+        "v_xad_u32", "v_pk_", "v_fma_f64", "v_add_f64", "v_mul_f64", "v_lshl_add_u64")
+QUARTER = ("v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_", "v_exp_", "v_log_", "v_div_")
+
+
+def slots(op):
+    if op.startswith(QUARTER):
+        return 4
+    if op.startswith(HALF):
+        return 2
+    return 1
+
+
 def classify(op):
     if op.startswith("v_"):
         return "valu"
@@ -34,8 +51,8 @@ def main():
             break
         m = re.match(r"^(\.LBB[^:]+|_Z[^:]+):", s)
         if m:
-            cur = {"name": m.group(1), "valu": 0, "salu": 0, "smem": 0, "lds": 0, "vmem": 0,
-                   "wait": 0, "ops": []}
+            cur = {"name": m.group(1), "valu": 0, "slots": 0, "salu": 0, "smem": 0, "lds": 0,
+                   "vmem": 0, "wait": 0, "ops": []}
             blocks.append(cur)
             continue
         if not s or s.startswith((";", ".")) or cur is None:
@@ -45,11 +62,13 @@ def main():
         if c:
             cur[c] += 1
             cur["ops"].append(op)
-    tot = {k: sum(b[k] for b in blocks) for k in ("valu", "salu", "smem", "lds", "vmem")}
+            if c == "valu":
+                cur["slots"] += slots(op)
+    tot = {k: sum(b[k] for b in blocks) for k in ("valu", "slots", "salu", "smem", "lds", "vmem")}
     print("total", tot, "blocks", len(blocks))
     for b in blocks:
         br = [o for o in b["ops"] if o.startswith("s_cbranch") or o == "s_branch"]
-        print(f"{b['name']:24s} valu {b['valu']:4d} salu {b['salu']:3d} smem {b['smem']:3d} "
+        print(f"{b['name']:24s} valu {b['valu']:4d} slots {b['slots']:4d} salu {b['salu']:3d} smem {b['smem']:3d} "
               f"lds {b['lds']:2d} vmem {b['vmem']:2d}  {' '.join(br)}")
 
 
