@@ -1,0 +1,46 @@
+#!/usr/bin/env bash
+# Round-3 measurement session on the GPU box (in-tree build): GPU tests, the C3 rocprofv3 session
+# (kernel trace + separate PMC passes, scripts/profile.sh), instruction-class PMC passes for C3 and
+# C5, and the bench lines of every config (C2-C5, with their CPU baselines).
+#   STEPS=(pytest profile classes bench) selects parts; each GPU step has its own time limit and the
+#   script stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+PARTS=${PARTS:-"pytest profile classes bench"}
+has() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
+if has pytest; then
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest -m gpu exit $rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has profile; then
+  bash scripts/profile.sh r03 || exit $?
+fi
+if has classes; then
+  for cfg in c3 c5; do
+    mkdir -p gpurun_out/cls_$cfg
+    args="--steps 2 --warmup 1 --no-cpu-baseline --config $cfg"
+    [ $cfg = c5 ] && args="$args --spp 256"
+    i=0
+    for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM" \
+               "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE" \
+               "SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FLOPS_FP32" \
+               "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT" ; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/cls_$cfg/p$i -o p$i \
+        -- python3 bench.py $args > gpurun_out/cls_$cfg/p$i.log 2>&1; rc=$?
+      echo "$cfg class pass $i exit $rc"; [ $rc -eq 0 ] || exit $rc
+    done
+    python3 scripts/pmc_summary.py gpurun_out/cls_$cfg > gpurun_out/cls_$cfg/summary.json
+  done
+fi
+if has bench; then
+  for cfg in c3 c2 c4 c5; do
+    st=5; [ $cfg = c4 ] && st=3; [ $cfg = c5 ] && st=2
+    timeout -k 10 420 python bench.py --config $cfg --steps $st --warmup 1 \
+      > gpurun_out/r03_bench_$cfg.json 2> gpurun_out/r03_bench_$cfg.err
+    rc=$?; echo "bench $cfg exit $rc"; [ $rc -eq 0 ] || exit $rc
+  done
+fi

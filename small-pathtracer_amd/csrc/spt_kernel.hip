@@ -33,6 +33,7 @@
 #include "../../include/spt_flops.h"
 #include "spt_device.h"
 #include "spt_cornell.h"
+#include "spt_diag.h"
 
 namespace spt {
 
@@ -56,7 +57,7 @@ constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the 
 #define SPT_SMALL_UNITS 1.5
 #endif
 #ifndef SPT_STEAL_MIN
-#define SPT_STEAL_MIN 1  // unstarted samples a donor must hold (in-wave stealing)
+#define SPT_STEAL_MIN 8  // unstarted samples a donor must hold (in-wave stealing; A/B in DESIGN.md §4)
 #endif
 #ifdef SPT_WAVE_TIMES
 constexpr int kStatWords = 32 + 3 * 32768;  // diagnostic: per-wave start, end, iterations
@@ -383,7 +384,6 @@ __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   return RectHit{tt, (bool)((int)ia & (int)ib), a};
 }
 
-struct alignas(16) SphLds { float px, py, pz, rad2; };  // a narrow sphere's LDS copy
 template <class SP>
 __device__ __forceinline__ float sphere_t(const SP& S, f3 o, f3 d) {
   // Sphere::intersect :229-239 in the reference's own form det = b^2 - op.op + r^2 (:233), as
@@ -428,19 +428,14 @@ __device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; 
 
 // The uploaded scene's rect tests are read from an LDS copy staged once per block (ds_read
 // broadcasts into VGPRs) -- the north star's "geometry staged once into LDS". A/B (DESIGN.md
-// section 4, scripts/ab_r02g.sh): faster than scalar loads through the constant address space
-// (-DSPT_GEO_SLOAD): generic kernel at C3 27.65 -> 26.26 ms, HEAD-topology kernel 19.1 -> 18.5 ms,
-// C5 at 256 spp 460 -> 453.6 ms. Spheres stay on scalar loads (an LDS copy, -DSPT_SPH_LDS, cost
-// C5 1.4 %: four VGPRs per unrolled sphere). The HEAD scene itself runs with its bounds as
-// instruction literals (15.5 ms).
+// section 4, round 2 at commit 407a07d): faster than scalar loads through the constant address
+// space: generic kernel at C3 27.65 -> 26.26 ms, HEAD-topology kernel 19.1 -> 18.5 ms, C5 at
+// 256 spp 460 -> 453.6 ms. Spheres stay on scalar loads (an LDS copy cost C5 1.4 %: four VGPRs per
+// unrolled sphere). The HEAD scene itself runs with its bounds as instruction literals (15.5 ms).
 // (the fp64 wide-sphere kernel keeps scalar loads: its VGPR budget is the tight one, 78 vs 90)
 template <class TP>
 __device__ __forceinline__ auto tests_of(const SPT_CONST SceneGeo* G, const GeoTest* lds) {
-#ifdef SPT_GEO_SLOAD
-  constexpr bool kLds = false;
-#else
   constexpr bool kLds = !TP::WIDE;
-#endif
   if constexpr (TP::CONSTGEO) {
     (void)G; (void)lds;
     return (const SPT_CONST GeoTest*)nullptr;  // the HEAD tests are literals (kCornellTests)
@@ -452,11 +447,6 @@ __device__ __forceinline__ auto tests_of(const SPT_CONST SceneGeo* G, const GeoT
     return G->test + 0;
   }
 }
-#ifdef SPT_SPH_LDS
-#define SPT_SPHS(G) s_sph
-#else
-#define SPT_SPHS(G) (G)->sph
-#endif
 template <class TP, class GP, class GT, class SP>
 __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect, GT tests,
                                                 SP sphs, const int* pos2idx, f3 o, f3 d,
@@ -651,18 +641,6 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Cost probes (diagnostic builds, -DSPT_PROBE=<bitmask>): a region is computed a second time on
-// opaque copies of its inputs and the copy is selected under an always-false opaque predicate, so
-// the image and the path statistics are unchanged and the time difference is the region's
-// marginal cost. 1 Philox, 2 trace, 8 cosine, 16 camera.
-#ifndef SPT_PROBE
-#define SPT_PROBE 0
-#endif
-template <typename T>
-__device__ __forceinline__ T opq(T v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
 
 // One lane = one pixel-sample path at a time, and every iteration traces exactly ONE ray per lane
 // with the same nearest-hit loop (intersect :323-335): either the path ray toward the next vertex
@@ -695,9 +673,6 @@ render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
   __shared__ GeoTest s_test[TP::CONSTGEO || TP::WIDE ? 1 : kMaxPrims];
-#ifdef SPT_SPH_LDS
-  __shared__ SphLds s_sph[TP::SPH ? kMaxPrims : 1];
-#endif
   // Pending REFR refraction children (:494-495 at depth <= 2), two per lane at most (MAT only):
   // o, d, T, depth, branch.
   struct Node { float o[3], d[3], T[3]; int depth; uint32_t branch; };
@@ -721,12 +696,6 @@ render_kernel(const KParams* __restrict__ Pg) {
         const SPT_CONST GeoTest& q = G->test[i];
         s_test[i] = GeoTest{q.k0, q.k1, q.ma, q.ha, q.mb, q.hb, q.pos0, q.pos1};
       }
-#ifdef SPT_SPH_LDS
-      if (TP::SPH && i < G->n_sph) {
-        const SPT_CONST GeoSph& q = G->sph[i];
-        s_sph[i] = SphLds{q.px, q.py, q.pz, q.rad2};
-      }
-#endif
     }
   }
   __syncthreads();
@@ -774,12 +743,8 @@ render_kernel(const KParams* __restrict__ Pg) {
   constexpr bool kNeeByIdentity = CF::NEE == 1 && !TP::MAT;
   // Early NEE resolve (early_nee_proven): the HEAD NEE kernel only. The shadow-ray resolve then
   // runs after the shading block, for the rays traced in this iteration and the proven ones.
-#ifdef SPT_NO_EARLY_NEE  // A/B builds only
-  constexpr bool kEarlyNee = false;
-#else
   constexpr bool kEarlyNee = TP::CONSTGEO && !TP::MAT && !TP::SPH && CF::NEE == 1 &&
                              CF::BLACK == 1 && CF::LREF == 1 && CF::MAXD0 == 1;
-#endif
   // The sphere NEE kernel (C5): the same early resolve with the sphere-scene predicate.
   constexpr bool kEarlySph = !kEarlyNee && TP::SPH && !TP::MAT && !TP::WIDE && CF::NEE == 1 &&
                              CF::BLACK == 1 && CF::LREF == 1;
@@ -805,22 +770,6 @@ render_kernel(const KParams* __restrict__ Pg) {
 #endif
     const SPT_CONST KParams* P = cptr(Pg);
     SPT_REGION(0);  // loop iteration
-#if defined(SPT_EXTRA_SALU) || defined(SPT_EXTRA_VALU)
-    {  // marginal-cost probes (A/B builds only): N extra SALU / VALU per iteration, results unused
-#ifdef SPT_EXTRA_SALU
-      uint64_t sd = (uint64_t)iter;
-#pragma unroll
-      for (int q = 0; q < SPT_EXTRA_SALU; ++q) asm volatile("s_and_b64 %0, %0, %0" : "+s"(sd) :: "scc");
-      asm volatile("" ::"s"(sd));
-#endif
-#ifdef SPT_EXTRA_VALU
-      float dv = fx;
-#pragma unroll
-      for (int q = 0; q < SPT_EXTRA_VALU; ++q) asm volatile("v_fma_f32 %0, %0, %0, %0" : "+v"(dv));
-      asm volatile("" ::"v"(dv));
-#endif
-    }
-#endif
     if (iter >= kMaxWaveIters) {  // runaway guard: drop the work, leave through the normal exit
       capped = true;                // (a second loop exit would duplicate the loop state)
       exhausted = true;
@@ -864,7 +813,6 @@ render_kernel(const KParams* __restrict__ Pg) {
       pool_next += min((uint32_t)__popcll(need), avail);
       need = __ballot(needs_unit);
     }
-#ifndef SPT_NO_STEAL
     // 2b) the queue is dry: an idle lane takes the upper half of a busy lane's unstarted samples
     //     (same pixel; each flushes its own sums and the accumulation is integer, so the image is
     //     unchanged). A wave's tail is then ~one path instead of ~one unit. Pairs are made by a
@@ -903,7 +851,6 @@ render_kernel(const KParams* __restrict__ Pg) {
         }
       }
     }
-#endif
     if (__ballot(ls != kStIdle) == 0) break;
     n_cos += (uint32_t)__popcll(__ballot(ls == kStCos));
 
@@ -918,17 +865,9 @@ render_kernel(const KParams* __restrict__ Pg) {
       if (ls != kStSpec) SPT_REGION(cam ? 3 : 8);
       const bool unit = unit_dirs_of<TP>(Pg);
       f3 v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0, unit);
-      if (SPT_PROBE & 8) {
-        const f3 v2 = cosine_vec<!TP::SPH>(nl, opq(r.z), r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0, unit);
-        if (opq(0u) != 0u) v = v2;
-      }
       // the vertex this ray leads to: depth + 1 (depth == 0 for a new sample's camera ray)
       const uint32_t ctr2 = ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u);
       r = philox_px(pk, s, ctr2);
-      if (SPT_PROBE & 1) {
-        const u4 r2 = philox_px(PxKey{opq(pk.qhi), pk.qlo, pk.lo}, s, ctr2);
-        if (opq(0u) != 0u) r = r2;
-      }
       {
         const SPT_CONST KParams* C = cptr(Pg);
         f3 vc;
@@ -965,13 +904,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
       int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
       float t, ia_hit;
-      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), SPT_SPHS(G), s_pos2idx, o, d, t, id, ia_hit);
-      if (SPT_PROBE & 2) {
-        float t2, ia2;
-        int id2 = id;
-        const bool h2 = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), SPT_SPHS(G), s_pos2idx, mk(opq(o.x), o.y, o.z), d, t2, id2, ia2);
-        if (opq(0u) != 0u) { hit = h2; t = t2; id = id2; ia_hit = ia2; }
-      }
+      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), G->sph, s_pos2idx, o, d, t, id, ia_hit);
 
       // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467). Then
       //    the light is the next vertex (shaded in the common block below, T = T*f*weight); else the
@@ -1801,11 +1734,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     const uint32_t waves = (uint32_t)(c->n_cu * c->bpc[kv] * (kBlock / 64));
     uint32_t sh = 1;  // 2^sh >= 2 x waves
     while ((1u << sh) < 2u * waves && sh < 31) ++sh;
-#ifdef SPT_GUIDED_ALWAYS  // A/B builds only
-    K.sh_guided = sh;
-#else
     K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
-#endif
   }
   K.chunk = chunk;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;

@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
 """Per-basic-block instruction mix of one kernel in a hipcc -S listing (static cost map).
 
-  python tools/isa_blocks.py build/spt_kernel.s render_kernelINS_4TopoILi6
+  python tools/isa_blocks.py build/spt_kernel.s render_kernelINS_4TopoILi6 [--bb] [--min N]
+
+--bb splits at LLVM's '; %bb.N' comments too (fall-through blocks), --min hides blocks with fewer
+VALU. `slots` weights each VALU by its issue cost on gfx950 (tools/valu_rates.hip,
+profiles/r01_valu_rates.txt): full-rate 1, half-rate 2, transcendental 4.
 """
 import re
 import sys
-
+from collections import Counter
 
 # Issue cost in VALU slots (one slot = a full-rate wave64 instruction, 2 cycles on a SIMD-32),
 # measured by tools/valu_rates.hip (profiles/r01_valu_rates.txt): half-rate ops 2, transcendental 4.
@@ -40,19 +44,20 @@ def classify(op):
     return None
 
 
-def main():
-    path, key = sys.argv[1], sys.argv[2]
+def blocks_of(path, key, bb=False):
     lines = open(path).read().splitlines()
-    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and key in l and ":" in l and not l.startswith("\t"))
+    start = next(i for i, l in enumerate(lines)
+                 if l.startswith("_Z") and key in l and ":" in l and not l.startswith("\t"))
     blocks, cur = [], None
     for l in lines[start:]:
         s = l.strip()
         if s == "s_endpgm":
             break
         m = re.match(r"^(\.LBB[^:]+|_Z[^:]+):", s)
-        if m:
-            cur = {"name": m.group(1), "valu": 0, "slots": 0, "salu": 0, "smem": 0, "lds": 0,
-                   "vmem": 0, "wait": 0, "ops": []}
+        m2 = re.match(r"^; (%bb\.\d+):", s) if bb else None
+        if m or m2:
+            cur = {"name": (m or m2).group(1)[:24], "valu": 0, "slots": 0, "salu": 0, "smem": 0,
+                   "lds": 0, "vmem": 0, "wait": 0, "ops": [], "vops": Counter()}
             blocks.append(cur)
             continue
         if not s or s.startswith((";", ".")) or cur is None:
@@ -64,12 +69,25 @@ def main():
             cur["ops"].append(op)
             if c == "valu":
                 cur["slots"] += slots(op)
+                cur["vops"][op] += 1
+    return blocks
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    path, key = args[0], args[1]
+    bb = "--bb" in sys.argv
+    mn = int(sys.argv[sys.argv.index("--min") + 1]) if "--min" in sys.argv else 0
+    blocks = blocks_of(path, key, bb)
     tot = {k: sum(b[k] for b in blocks) for k in ("valu", "slots", "salu", "smem", "lds", "vmem")}
     print("total", tot, "blocks", len(blocks))
     for b in blocks:
+        if b["valu"] < mn:
+            continue
         br = [o for o in b["ops"] if o.startswith("s_cbranch") or o == "s_branch"]
-        print(f"{b['name']:24s} valu {b['valu']:4d} slots {b['slots']:4d} salu {b['salu']:3d} smem {b['smem']:3d} "
-              f"lds {b['lds']:2d} vmem {b['vmem']:2d}  {' '.join(br)}")
+        top = ", ".join(f"{k}:{v}" for k, v in b["vops"].most_common(4))
+        print(f"{b['name']:24s} valu {b['valu']:4d} slots {b['slots']:4d} salu {b['salu']:3d} "
+              f"smem {b['smem']:3d} lds {b['lds']:2d} vmem {b['vmem']:2d}  {' '.join(br)}  [{top}]")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-wave residency of a -DSPT_WAVE_TIMES build (SPT_WAVE_DUMP file): how much of the kernel's
+"""Per-wave residency of a -DSPT_DIAG=2 build (spt_diag.h: SPT_WAVE_TIMES) (SPT_WAVE_DUMP file): how much of the kernel's
 span the waves are resident, and how the last waves straggle (queue tail).
 
   python tools/wave_tail.py gpurun_out/waves_c2.bin
