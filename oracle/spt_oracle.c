@@ -724,9 +724,10 @@ static float c_sphere_wide(const c_prim* P, fv o, fv d) {
 }
 
 /* A narrow sphere in fp32: det = b^2 - op.op + r^2 (:233, as one fma), the nearest root beyond
- * the fp32 epsilon 2e-3; 0 = no hit. The root of det is det * rsq_nr(det) (the
- * contract's reciprocal square root, ~1e-7 relative; det = 0 gives 0), not an IEEE sqrtf: on the
- * GPU the correctly rounded square root is an ~18-slot sequence (C5: -5.6 %). Pinned against the
+ * the fp32 epsilon 2e-3; 0 = no hit. The root of det is det * rsq_nr2(det) (the contract's
+ * reciprocal square root with two Newton steps, 5e-6 relative: 3e-5 in t at r = 6, far below the
+ * epsilon; det = 0 gives 0), not an IEEE sqrtf: on the GPU the correctly rounded square root is an
+ * ~18-slot sequence, rsq_nr2 10 (round 2 took det * rsq_nr(det), 13). Pinned against the
  * reference's own fp64 Sphere by the sph/sph16 P2 runs. */
 static float c_sphere(const c_prim* P, fv o, fv d) {
   const fv op = fv3(P->px - o.x, P->py - o.y, P->pz - o.z);
@@ -734,7 +735,7 @@ static float c_sphere(const c_prim* P, fv o, fv d) {
   const float det = fmaf(bb, bb, P->rad2 - fdot(op, op)); /* :233's b*b - op.op + rad*rad */
   float sd, t1, t2;
   if (!(det >= 0.0f)) return 0.0f;
-  sd = det * spt_oracle_rsq_nr(det);
+  sd = det * spt_oracle_rsq_nr2(det); /* two Newton steps (round 3): 5e-6 relative */
   t1 = bb - sd;
   t2 = bb + sd;
   return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);

@@ -393,9 +393,11 @@ __device__ __forceinline__ float sphere_t(const SP& S, f3 o, f3 d) {
   const float bb = dot3(op, d);
   const float det = fmaf(bb, bb, S.rad2 - dot3(op, op));
   if (!(det >= 0.0f)) return 0.0f;
-  // the root as det * rsq_nr(det) (contract, oracle c_sphere): the IEEE sqrtf sequence costs ~18
-  // issue slots, this 13 (C5 at 256 spp 452.8 -> 427.3 ms); det = 0 gives 0
-  const float sd = det * rsq_nr(det);
+  // the root as det * rsq_nr2(det) (contract, oracle c_sphere): the IEEE sqrtf sequence costs ~18
+  // issue slots, det * rsq_nr(det) 13 (round 2: C5 at 256 spp 452.8 -> 427.3 ms), two Newton steps
+  // 10 (round 3: the root within 5e-6 relative, 3e-5 at r = 6, far below the 2e-3 epsilon);
+  // det = 0 gives 0
+  const float sd = det * rsq_nr2(det);
   const float t1 = bb - sd, t2 = bb + sd;
   return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
 }
