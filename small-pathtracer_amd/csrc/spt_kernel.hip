@@ -56,6 +56,9 @@ constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the 
 #ifndef SPT_SMALL_UNITS
 #define SPT_SMALL_UNITS 1.5
 #endif
+#ifndef SPT_SCRAMBLE_K
+#define SPT_SCRAMBLE_K 8  // pixel-order spreading factor of the work units (1 = off; A/B in DESIGN.md §4)
+#endif
 #ifndef SPT_STEAL_MIN
 #define SPT_STEAL_MIN 8  // unstarted samples a donor must hold (in-wave stealing; A/B in DESIGN.md §4)
 #endif
@@ -143,6 +146,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // lanes need, kGrabMin, left >> sh_guided)) units per queue atomic, left = units not yet handed
   // out, so no wave hoards a full pool while the queue runs dry. sh_guided = 32: always kGrab.
   uint32_t sh_guided;
+  uint32_t scr_k, scr_q;  // pixel-order spreading of the units: K = 2^scr_k, scr_q = npix / K
   float inv_spp, inv_w, inv_h;
   float fix_scale;  // inv_spp * 2^31 (fix31)
   // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
@@ -803,8 +807,13 @@ render_kernel(const KParams* __restrict__ Pg) {
       if (needs_unit && rank < avail) {
         const uint32_t u = pool_next + rank;
         const uint32_t npix = (uint32_t)Q->n_local_pix, w = (uint32_t)Q->width;
-        const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major: adjacent pixels
+        const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major
         lp = u - j * npix;
+        // Spread the pixel order (scr_k > 0): unit pixel lp = b * K + a -> a * (npix / K) + b, so a
+        // wave's run of consecutive units samples the whole image instead of one row segment, and
+        // per-wave work varies less (the image does not change: every pixel-sample is still done
+        // once and summed in integers)
+        lp = (lp & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (lp >> Q->scr_k);
         s = j * (uint32_t)Q->chunk;
         s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
         (void)w;
@@ -1745,6 +1754,10 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
   magic31((uint32_t)K.n_local_pix, &K.m_npix, &K.sh_npix);
+  // pixel-order spreading: the largest K = 2^k <= SPT_SCRAMBLE_K dividing n_local_pix
+  K.scr_k = 0;
+  while ((1 << (K.scr_k + 1)) <= SPT_SCRAMBLE_K && K.n_local_pix % (1 << (K.scr_k + 1)) == 0) ++K.scr_k;
+  K.scr_q = (uint32_t)K.n_local_pix >> K.scr_k;
   magic31((uint32_t)p->width, &K.m_w, &K.sh_w);
   magic31((uint32_t)K.tile_rows, &K.m_tile, &K.sh_tile);
   K.inv_spp = 1.0f / (float)p->spp;
