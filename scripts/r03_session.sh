@@ -19,16 +19,19 @@ if has profile; then
   bash scripts/profile.sh r03 || exit $?
 fi
 if has classes; then
-  for cfg in c3 c5; do
-    mkdir -p gpurun_out/cls_$cfg
+  # CLS: configurations (tag[:chunk]); c2:32 = C2 at 32-sample units (the C2 tail study)
+  for spec in ${CLS:-c3 c5}; do
+    cfg=${spec%%:*}; tag=$cfg
     args="--steps 2 --warmup 1 --no-cpu-baseline --config $cfg"
     [ $cfg = c5 ] && args="$args --spp 256"
+    case $spec in *:*) args="$args --chunk ${spec#*:}"; tag=${cfg}_u${spec#*:};; esac
+    mkdir -p gpurun_out/cls_$tag; cfg=$tag
     i=0
     for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM" \
                "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE" \
                "SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FLOPS_FP32" \
                "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT" ; do
-      i=$((i+1))
+      i=$((i+1)); [ $i -le ${CLS_PASSES:-4} ] || break
       timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/cls_$cfg/p$i -o p$i \
         -- python3 bench.py $args > gpurun_out/cls_$cfg/p$i.log 2>&1; rc=$?
       echo "$cfg class pass $i exit $rc"; [ $rc -eq 0 ] || exit $rc

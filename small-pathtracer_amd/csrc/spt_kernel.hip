@@ -1750,7 +1750,6 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.chunk = chunk;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
   const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
-  if (n_units >= 0xFFFF0000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
   magic31((uint32_t)K.n_local_pix, &K.m_npix, &K.sh_npix);
