@@ -358,6 +358,42 @@ def main() -> None:
         dist.broadcast_object_list(uid, src=0)
         comm = spt.Comm(uid[0], world, rank, local)
         comm.reserve(params)
+    gather_mode = "spt (RCCL send/recv)" if comm is not None else (
+        "torch (dist.gather)" if use_torch_gather else ("host (gloo)" if world > 1 else "none"))
+    if comm is not None:
+        # The library gather has not run on >1 GPU before the driver's scaling run: check it on a
+        # known pattern (every rank's rows, exact in fp32) before anything is timed, and fall back
+        # to torch's gather for the whole run if it raises or mismatches (recorded in the line).
+        ok, why = True, ""
+        try:
+            rr = torch.as_tensor(my_rows, device="cuda", dtype=torch.int64).view(-1, 1, 1)
+            xx = torch.arange(w, device="cuda", dtype=torch.int64).view(1, -1, 1)
+            cc = torch.arange(3, device="cuda", dtype=torch.int64).view(1, 1, -1)
+            shard.zero_()
+            shard[: len(my_rows)] = ((rr * 7 + xx * 3 + cc) % 65521).to(torch.float32)
+            if rank == 0:
+                full.fill_(-1.0)
+            comm.gather(params, shard.data_ptr(), full.data_ptr() if rank == 0 else 0,
+                        stream.cuda_stream)
+            torch.cuda.synchronize()
+            if rank == 0:
+                ra = torch.arange(h, device="cuda", dtype=torch.int64).view(-1, 1, 1)
+                want = ((ra * 7 + xx * 3 + cc) % 65521).to(torch.float32)
+                if not torch.equal(full, want):
+                    ok, why = False, "pattern mismatch"
+        except Exception as e:  # noqa: BLE001
+            ok, why = False, f"{type(e).__name__}: {e}"
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            log(f"bench.py: rank {rank}: library gather check failed ({why or 'on another rank'}); "
+                f"using torch.distributed.gather")
+            comm = None
+            use_torch_gather = True
+            slots = [torch.zeros_like(shard) for _ in range(world)] if rank == 0 else None
+            gather_mode = f"torch (dist.gather; library gather check failed: {why or 'another rank'})"
+        else:
+            gather_mode = "spt (RCCL send/recv; pattern check passed)"
     kstats = []
 
     def step():
@@ -468,7 +504,7 @@ def main() -> None:
                      if cfg["scene"] == "cornell" else
                      "synthetic: C5's 32-sphere scene (the room and light of smallpt.cpp:288-294 plus "
                      "32 DIFF spheres of the reference's Sphere class :223-254)")
-                    + " and camera (:521), Philox4x32-10 stream seed 1",
+                    + " and camera (:521), Philox4x32-7 stream seed 1",
             "config": {"workload": cfg["desc"] + (f", weak-scaled to {spp} spp over {world} GPUs"
                                                    if scaling == "weak" and world > 1 else ""),
                        "width": w, "height": h, "spp": spp,
@@ -504,6 +540,7 @@ def main() -> None:
                       "misses_per_sample": round(s0["misses"] / my_samples, 4)},
             "quality": qual,
             "gather_equals_1gpu_render": gather_exact,
+            "gather": gather_mode,
             "cpu_baseline": cpu,
             "image_writer": writer,
         }

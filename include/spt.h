@@ -79,7 +79,7 @@ typedef enum spt_light_mode { SPT_LIGHT_GLIBC_WRAP = 0, SPT_LIGHT_UNIFORM = 1 } 
 
 typedef struct spt_params {
   int32_t width, height, spp; /* :507-508 */
-  uint32_t seed;              /* Philox4x32-10 counter word 3 (the key is the fixed SPT_PHILOX_KEY) */
+  uint32_t seed;              /* Philox4x32-7 counter word 3 (the key is the fixed SPT_PHILOX_KEY) */
   float nee_prob;             /* Q of :464 (`q < Q`): 1 = HEAD explicit light sampling, 0 = cosine only */
   int32_t rr_depth;           /* Russian roulette starts when ++depth > rr_depth  (:448, HEAD = 5) */
   int32_t max_depth;          /* 0 = unbounded (reference); >0 = path ends at this vertex depth */

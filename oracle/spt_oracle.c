@@ -15,7 +15,7 @@
  *     (pinned against oracle/_ref in tests/test_oracle_golden.py and tests/golden/).
  *
  *  2. COUNTER mode (spt_oracle_counter_render): the device path's contract — the same algorithm in
- *     fp32 with a counter-based Philox4x32-10 stream (fixed key; counter = pixel, sample,
+ *     fp32 with a counter-based Philox4x32-7 stream (fixed key; counter = pixel, sample,
  *     vertex | stream << 31, seed),
  *     an iterative bounce loop and fixed-point per-pixel accumulation. Every float operation is
  *     spelled out (explicit fmaf, correctly rounded div/sqrt, own sincos polynomial) so that the HIP
@@ -423,7 +423,7 @@ double spt_oracle_prim_intersect(const spt_prim* s, const double o[3], const dou
 /* COUNTER MODE (fp32) — the device contract                                                   */
 /* ========================================================================================== */
 
-/* Philox4x32-10 (Salmon et al., SC'11; Random123 constants). */
+/* Philox4x32-R (Salmon et al., SC'11; Random123 constants): R = 10 for the KATs, SPT_PHILOX_ROUNDS = 7 in the contract. */
 #define PH_M0 0xD2511F53u
 #define PH_M1 0xCD9E8D57u
 #define PH_W0 0x9E3779B9u
