@@ -16,7 +16,7 @@
 //   * a NEE shadow ray is traced only if the light's own test accepts it; in the reference's room
 //     the HEAD NEE kernel resolves most of those at once, where an exact geometric predicate
 //     proves that nothing lies between the vertex and the light (early_nee_proven);
-//   * Philox4x32-10 counter RNG keyed by (seed; pixel, sample, vertex, stream);
+//   * Philox4x32-7 counter RNG keyed by (seed; pixel, sample, vertex, stream);
 //   * per-pixel accumulation in 1.31 fixed point with 64-bit integer atomics: exact, independent
 //     of unit size, lane order, queue order, stealing and GPU count.
 #include <hip/hip_runtime.h>
@@ -58,6 +58,11 @@ constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the 
 #endif
 #ifndef SPT_SCRAMBLE_K
 #define SPT_SCRAMBLE_K 8  // pixel-order spreading factor of the work units (1 = off; A/B in DESIGN.md §4)
+#endif
+#ifndef SPT_UNIT_SLOTS
+// 1: a unit's owner lane stores its three sums to the unit's own slot (plain stores, no atomics);
+// only stolen ranges add into the per-pixel accumulator; finalize_kernel sums both
+#define SPT_UNIT_SLOTS 1
 #endif
 #ifndef SPT_STEAL_MIN
 #define SPT_STEAL_MIN 8  // unstarted samples a donor must hold (in-wave stealing; A/B in DESIGN.md §4)
@@ -159,7 +164,8 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   float early_y0;
   int unit_dirs;  // oracle c_unit_dirs: the scene has a sphere or a REFR primitive
   float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
-  unsigned long long* accum;  // [n_local_pix][3] 32.32 fixed point
+  unsigned long long* accum;  // [n_local_pix][3] 1.31 fixed point (stolen ranges; every unit without slots)
+  unsigned long long* slots;  // [n_units][3] one owner store per unit, unit order (SPT_UNIT_SLOTS)
   uint32_t* queue;            // [0] = next unit
   unsigned long long* stats;  // [8]
 };
@@ -818,6 +824,9 @@ render_kernel(const KParams* __restrict__ Pg) {
         s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
         (void)w;
         pixel_terms(Q, lp, pk, fx, fy);
+#if SPT_UNIT_SLOTS
+        lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
+#endif
         ls = kStCam;
         needs_unit = false;
       }
@@ -843,7 +852,15 @@ render_kernel(const KParams* __restrict__ Pg) {
           const uint32_t dcur = (uint32_t)__builtin_amdgcn_readlane((int)cur, dl);
           const uint32_t dend = (uint32_t)__builtin_amdgcn_readlane((int)s_end, dl);
           const uint32_t mid = dcur + (dend - dcur) / 2u;  // donor keeps [.., mid), taker [mid, dend)
-          const uint32_t d_lp = (uint32_t)__builtin_amdgcn_readlane((int)lp, dl);
+          uint32_t d_lp = (uint32_t)__builtin_amdgcn_readlane((int)lp, dl);
+#if SPT_UNIT_SLOTS
+          if (d_lp >> 31) {  // an owner donor holds its unit index: the taker adds by pixel
+            const SPT_CONST KParams* Q = cptr(Pg);
+            const uint32_t du = d_lp & 0x7FFFFFFFu;
+            const uint32_t r = du - div_magic(du, Q->m_npix, Q->sh_npix) * (uint32_t)Q->n_local_pix;
+            d_lp = (r & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (r >> Q->scr_k);
+          }
+#endif
           const uint32_t d_qhi = (uint32_t)__builtin_amdgcn_readlane((int)pk.qhi, dl);
           const uint32_t d_qlo = (uint32_t)__builtin_amdgcn_readlane((int)pk.qlo, dl);
           const uint32_t d_lo = (uint32_t)__builtin_amdgcn_readlane((int)pk.lo, dl);
@@ -1189,10 +1206,20 @@ render_kernel(const KParams* __restrict__ Pg) {
           ls = kStCam;
           if (s >= s_end) {  // the unit's last sample: flush its pixel's fixed-point sums
             SPT_REGION(1);
-            unsigned long long* a = cptr(Pg)->accum + 3ull * lp;
-            if (acc0) atomicAdd(a + 0, acc0);
-            if (acc1) atomicAdd(a + 1, acc1);
-            if (acc2) atomicAdd(a + 2, acc2);
+#if SPT_UNIT_SLOTS
+            if (lp >> 31) {  // the unit's owner: its slot, written exactly once (zeros included)
+              unsigned long long* a = cptr(Pg)->slots + 3ull * (lp & 0x7FFFFFFFu);
+              a[0] = acc0;
+              a[1] = acc1;
+              a[2] = acc2;
+            } else
+#endif
+            {
+              unsigned long long* a = cptr(Pg)->accum + 3ull * lp;
+              if (acc0) atomicAdd(a + 0, acc0);
+              if (acc1) atomicAdd(a + 1, acc1);
+              if (acc2) atomicAdd(a + 2, acc2);
+            }
             acc0 = acc1 = acc2 = 0;
             ls = kStIdle;
           }
@@ -1288,6 +1315,28 @@ finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict_
     rgb[i] = v > 1.0f ? 1.0f : v;
   }
 }
+// The same with the unit slots: thread t takes unit-order pixel t (coalesced slot reads, chunk
+// j's slot at j * npix + t), adds the pixel's stolen-range sums and writes its spread pixel
+// p = (t mod K) * (npix / K) + t / K. Integer sums: the order of the adds cannot matter.
+__global__ void __launch_bounds__(kBlock)
+finalize_slots_kernel(const unsigned long long* __restrict__ accum,
+                      const unsigned long long* __restrict__ slots, float* __restrict__ rgb,
+                      uint32_t npix, uint32_t n_chunks, uint32_t scr_k, uint32_t scr_q) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= npix) return;
+  const uint32_t p = (t & ((1u << scr_k) - 1u)) * scr_q + (t >> scr_k);
+  unsigned long long v0 = accum[3ull * p], v1 = accum[3ull * p + 1], v2 = accum[3ull * p + 2];
+  for (uint32_t j = 0; j < n_chunks; ++j) {
+    const unsigned long long* q = slots + 3ull * ((size_t)j * npix + t);
+    v0 += q[0];
+    v1 += q[1];
+    v2 += q[2];
+  }
+  const float f0 = (float)v0 * 0x1p-31f, f1 = (float)v1 * 0x1p-31f, f2 = (float)v2 * 0x1p-31f;
+  rgb[3ull * p] = f0 > 1.0f ? 1.0f : f0;
+  rgb[3ull * p + 1] = f1 > 1.0f ? 1.0f : f1;
+  rgb[3ull * p + 2] = f2 > 1.0f ? 1.0f : f2;
+}
 
 }  // namespace spt
 
@@ -1330,6 +1379,8 @@ struct spt_context {
   SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
   size_t accum_cap = 0;  // elements
+  unsigned long long* slots = nullptr;  // [n_units][3] (SPT_UNIT_SLOTS), grown on demand
+  size_t slots_cap = 0;                 // elements
   uint32_t* queue = nullptr;
   unsigned long long* stats = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1573,6 +1624,7 @@ extern "C" spt_status spt_context_destroy(spt_context* c) {
   if (c->d_kp) (void)hipFree(c->d_kp);
   if (c->h_kp) (void)hipHostFree(c->h_kp);
   if (c->accum) (void)hipFree(c->accum);
+  if (c->slots) (void)hipFree(c->slots);
   if (c->queue) (void)hipFree(c->queue);
   if (c->stats) (void)hipFree(c->stats);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1764,6 +1816,16 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.inv_w = 1.0f / (float)p->width;
   K.inv_h = 1.0f / (float)p->height;
   K.accum = c->accum;
+#if SPT_UNIT_SLOTS
+  if (3ull * n_units > c->slots_cap) {  // one owner store per unit (24 B): C3 208 MB, C4/C5 ~400 MB
+    if (c->slots) SPT_HIP(hipFree(c->slots));
+    c->slots = nullptr;
+    c->slots_cap = 0;
+    SPT_HIP(hipMalloc(&c->slots, 3ull * n_units * sizeof(unsigned long long)));
+    c->slots_cap = 3ull * n_units;
+  }
+#endif
+  K.slots = c->slots;
   K.queue = c->queue;
   K.stats = c->stats;
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
@@ -1797,9 +1859,16 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                      (const KParams*)c->d_kp);
   SPT_HIP(hipGetLastError());
   SPT_HIP(hipEventRecord(c->ev1, stream));
+#if SPT_UNIT_SLOTS
+  const uint32_t np = (uint32_t)K.n_local_pix;
+  hipLaunchKernelGGL(finalize_slots_kernel, dim3((np + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                     (const unsigned long long*)c->accum, (const unsigned long long*)c->slots,
+                     rgb_dev, np, (uint32_t)n_chunks, K.scr_k, K.scr_q);
+#else
   const uint32_t n = 3u * (uint32_t)K.n_local_pix;
   hipLaunchKernelGGL(finalize_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
                      (const unsigned long long*)c->accum, rgb_dev, n);
+#endif
   SPT_HIP(hipGetLastError());
   c->pending = true;
   return SPT_OK;
