@@ -264,7 +264,8 @@ def main() -> None:
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
     ap.add_argument("--spp", type=int, default=0, help="override spp (per-GPU for weak scaling)")
-    ap.add_argument("--chunk", type=int, default=0, help="samples per work unit (0 = auto)")
+    ap.add_argument("--chunk", type=int, default=int(os.environ.get("SPT_CHUNK", "0")),
+                    help="samples per work unit (0 = auto; A/B scripts set SPT_CHUNK)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
