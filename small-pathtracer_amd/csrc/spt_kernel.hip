@@ -47,7 +47,16 @@ constexpr int kBlock = 256;
 #define SPT_GRAB 64
 #endif
 constexpr uint32_t kGrab = SPT_GRAB;
-constexpr uint32_t kGrabMin = 16;  // guided grabs never take fewer (bounds the queue atomics)
+// Guided grabs of short launches: left >> (log2(2 x waves) + SPT_GUIDED_EXTRA) units, at least
+// SPT_GRAB_MIN. Round 3 (C2, 8 rounds on two boxes): 16 / +0 -> 8 / +1 cut the kernel 1.0-1.6 %;
+// 8 / +0, 4 / +0, 16 / +1 and 4 / +2 did not (profiles/r03_ab.txt session 10).
+#ifndef SPT_GRAB_MIN
+#define SPT_GRAB_MIN 8
+#endif
+#ifndef SPT_GUIDED_EXTRA
+#define SPT_GUIDED_EXTRA 1
+#endif
+constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (bounds the queue atomics)
 // Launches with fewer lane-iterations per resident lane than SPT_SMALL_ITERS deal their units
 // almost all at once (SPT_SMALL_UNITS per lane) and balance by stealing (host, spt_render_async).
 #ifndef SPT_SMALL_ITERS
@@ -1797,6 +1806,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     const uint32_t waves = (uint32_t)(c->n_cu * c->bpc[kv] * (kBlock / 64));
     uint32_t sh = 1;  // 2^sh >= 2 x waves
     while ((1u << sh) < 2u * waves && sh < 31) ++sh;
+    sh = std::min(31u, sh + (uint32_t)SPT_GUIDED_EXTRA);
     K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
   }
   K.chunk = chunk;
