@@ -1807,7 +1807,10 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     uint32_t sh = 1;  // 2^sh >= 2 x waves
     while ((1u << sh) < 2u * waves && sh < 31) ++sh;
     sh = std::min(31u, sh + (uint32_t)SPT_GUIDED_EXTRA);
-    K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
+#ifndef SPT_GUIDED_ALL
+#define SPT_GUIDED_ALL 0  // A/B: guided grabs for long launches too
+#endif
+    K.sh_guided = (small_launch || SPT_GUIDED_ALL) ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
   }
   K.chunk = chunk;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
