@@ -72,8 +72,29 @@ __device__ __forceinline__ int dev_toInt(const float* __restrict__ thr, float x)
   return v;
 }
 
-__device__ __forceinline__ uint32_t text_len(int v) {
-  return v < 0 ? 12u : v >= 100 ? 4u : v >= 10 ? 3u : 2u;  // digits + the trailing space
+// The same without branches (both table words read, selects instead of the if/else): one straight
+// block per value instead of three exec-masked ones (round 3: the branchy form cost ~39 SALU per
+// wave-value in the P3 encoder).
+__device__ __forceinline__ int dev_toInt_bf(const float* __restrict__ thr, float x) {
+  const float xc = fminf(fmaxf(x, 0.0f), 1.0f);
+  const float est = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(xc) * (1.0f / 2.2f)) * 255.0f + 0.5f;
+  const int v = (int)fminf(fmaxf(est, 0.0f), 255.0f);
+  const float hi = thr[min(v + 1, 255)], lo = thr[v];
+  const int inc = (int)(v < 255) & (int)(x >= hi), dec = (inc ^ 1) & (int)(x < lo);
+  return x != x ? (int)0x80000000 : v + inc - dec;
+}
+
+// "%d " of v in [0, 255] as one little-endian word of n = 2..4 bytes: the 3-digit text
+// "hdd " shifted right past its leading zero digits (v / 10 as (v * 205) >> 11, exact below 1029).
+__device__ __forceinline__ uint32_t text_word(int v, uint32_t& n) {
+  const uint32_t u = (uint32_t)v, t = (u * 205u) >> 11, d0 = u - t * 10u;
+  const uint32_t h = (t * 205u) >> 11, d1 = t - h * 10u;
+  n = 2u + (uint32_t)(u >= 10u) + (uint32_t)(u >= 100u);
+  return (0x20303030u + (h | d1 << 8 | d0 << 16)) >> (32u - 8u * n);
+}
+
+__device__ __forceinline__ uint32_t text_len(int v) {  // digits + the trailing space; -1: no value
+  return v == -1 ? 0u : v < 0 ? 12u : v >= 100 ? 4u : v >= 10 ? 3u : 2u;
 }
 
 __device__ __forceinline__ uint32_t put_value(uint8_t* p, int v) {  // "%d " into LDS
@@ -122,7 +143,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
 // look-back always makes progress. status[b] = flag << 62 | value: flag 1 = the block's own
 // aggregate, 2 = its inclusive prefix (header included). Agent-scope atomics on the status words
 // keep the hand-off coherent across the XCDs' L2s.
-constexpr int kStageP3 = kPixPerBlock * 3 * 4 + 16;  // every value of a block <= "255 ": 12 KB
+constexpr int kStageP3 = kPixPerBlock * 3 * 4 + 32;  // every value <= "255 ": 24 KB + the phase
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
 
 // Relaxed agent-scope atomics: the status word is the only datum that crosses blocks (no other
@@ -141,10 +162,13 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
           uint64_t cap, uint64_t* __restrict__ total_out) {
   __shared__ float s_thr[256];
   __shared__ uint32_t s_wave[kThreads / 64];
-  __shared__ __attribute__((aligned(16))) uint8_t s_txt[kStageP3];
+  __shared__ __attribute__((aligned(16))) uint32_t s_dw[kStageP3 / 4];
+  uint8_t* const s_txt = (uint8_t*)s_dw;
   __shared__ uint32_t s_bid;
   __shared__ uint64_t s_prefix;
   if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
+  for (int i = threadIdx.x; i < kStageP3 / 16; i += kThreads)  // the OR-assembled staging starts at 0
+    ((uint4*)s_dw)[i] = make_uint4(0u, 0u, 0u, 0u);
   load_thr(s_thr, T);  // barrier
   const uint32_t bid = s_bid;
   const uint64_t b0 = (uint64_t)bid * kPixPerBlock * 3, nv = (uint64_t)n_pix * 3;
@@ -161,14 +185,18 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
 #pragma unroll
     for (int i = 0; i < kPixPerThread * 3; ++i) x[i] = v0 + i < nv ? rgb[v0 + i] : 0.0f;
   }
+  // toInt values; -1 marks a slot past the image's end (no text), INT_MIN a NaN (12 bytes)
   int vals[kPixPerThread * 3];
   uint32_t len = 0;
+  bool nan = false;
 #pragma unroll
   for (int i = 0; i < kPixPerThread * 3; ++i) {
-    const bool in = v0 + i < nv;
-    vals[i] = in ? dev_toInt(s_thr, x[i]) : 0;
-    len += in ? text_len(vals[i]) : 0u;
+    const int v = dev_toInt_bf(s_thr, x[i]);
+    vals[i] = v0 + i < nv ? v : -1;
+    nan |= vals[i] == (int)0x80000000;
+    len += text_len(vals[i]);
   }
+  const bool block_nan = __syncthreads_or(nan) != 0;
   uint32_t total;
   const uint32_t my = block_excl_scan(len, s_wave, &total);
   if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors per step
@@ -211,11 +239,11 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   }
   __syncthreads();
   const uint64_t dst = s_prefix;
-  if (total + 16 > (uint32_t)kStageP3) {  // NaN-heavy block: direct byte stores, no staging
+  if (block_nan || total + 32 > (uint32_t)kStageP3) {  // a NaN (12-byte text): direct byte stores
     uint64_t q = dst + my;
 #pragma unroll
     for (int i = 0; i < kPixPerThread * 3; ++i) {
-      if (v0 + i >= nv) break;
+      if (vals[i] == -1) break;
       uint8_t b[12];
       const uint32_t n = put_value(b, vals[i]);
       for (uint32_t k = 0; k < n; ++k, ++q)
@@ -223,29 +251,47 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
     }
     return;
   }
-  const uint32_t phase = (uint32_t)(dst & 3u);  // stage at the destination's dword phase
-  uint8_t* p = s_txt + phase + my;
+  // Stage the block's text at the destination's 16-byte phase. Each value's text (2-4 bytes) is
+  // appended to a 64-bit accumulator at the thread's byte offset and its low dword ORed into the
+  // zeroed staging after every value (ds_or: a thread's first and last dword are shared with its
+  // neighbours; re-ORing a growing dword is idempotent); the dword index advances once 32 bits are
+  // full. Branch-free: a few VALU and one LDS op per value.
+  const uint32_t phase = (uint32_t)(dst & 15u);
+  const uint32_t o = phase + my;
+  uint32_t di = o >> 2, nb = (o & 3u) * 8u;
+  uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < kPixPerThread * 3; ++i)
-    if (v0 + i < nv) p += put_value(p, vals[i]);
+  for (int i = 0; i < kPixPerThread * 3; ++i) {
+    uint32_t n;
+    const uint32_t wv = text_word(max(vals[i], 0), n);
+    acc |= (uint64_t)wv << nb;
+    nb += vals[i] < 0 ? 0u : 8u * n;  // -1: past the image's end
+    atomicOr(&s_dw[di], (uint32_t)acc);
+    const uint32_t full = nb >> 5;  // 0 or 1
+    acc = full ? acc >> 32 : acc;
+    nb -= full << 5;
+    di += full;
+  }
+  if (nb) atomicOr(&s_dw[di], (uint32_t)acc);
   __syncthreads();
   if (dst + total > cap) {  // the host reports the error; write nothing past cap
     for (uint32_t i = threadIdx.x; i < total; i += kThreads)
       if (dst + i < cap) out[dst + i] = s_txt[phase + i];
     return;
   }
-  const uint64_t a0 = (dst + 3u) & ~3ull, a1 = (dst + total) & ~3ull;
+  const uint64_t a0 = (dst + 15u) & ~15ull, a1 = (dst + total) & ~15ull;
   if (a0 >= a1) {
     for (uint32_t i = threadIdx.x; i < total; i += kThreads) out[dst + i] = s_txt[phase + i];
     return;
   }
+  // 16-byte stores: the staging sits at the destination's 16-byte phase, so phase + head is 0 or 16
   const uint32_t head = (uint32_t)(a0 - dst), tail = (uint32_t)(dst + total - a1);
   if (threadIdx.x < head) out[dst + threadIdx.x] = s_txt[phase + threadIdx.x];
   if (threadIdx.x < tail) out[a1 + threadIdx.x] = s_txt[phase + (uint32_t)(a1 - dst) + threadIdx.x];
-  const uint32_t n_dw = (uint32_t)((a1 - a0) >> 2);
-  const uint32_t* s_dw = (const uint32_t*)(s_txt + phase + head);
-  uint32_t* o_dw = (uint32_t*)(out + a0);
-  for (uint32_t i = threadIdx.x; i < n_dw; i += kThreads) o_dw[i] = s_dw[i];
+  const uint32_t n_q = (uint32_t)((a1 - a0) >> 4);
+  const uint4* s_q = (const uint4*)(s_txt + phase + head);
+  uint4* o_q = (uint4*)(out + a0);
+  for (uint32_t i = threadIdx.x; i < n_q; i += kThreads) o_q[i] = s_q[i];
 }
 
 // P6: header (padded to 16 bytes, see header()), then toInt bytes (the int's low byte, as a
