@@ -3,10 +3,10 @@
 //
 // The reference writes `fprintf(f, "%d %d %d ", toInt(r), toInt(g), toInt(b))` per pixel: ASCII
 // P3, 6-12 bytes per pixel, ~200 MB of text at 4096². Here the framebuffer never leaves HBM until
-// the bytes are final, in ONE HBM-bound pass (p3_single): each 2048-pixel block loads its values
-// with float4 loads, formats 8 pixels per thread, finds its byte offset by a block scan plus a
-// decoupled look-back over its predecessors' published lengths, stages its text in LDS at the
-// destination's dword phase and writes it with aligned dword stores (head/tail bytes apart).
+// the bytes are final, in ONE HBM-bound pass (p3_single): each 4096-pixel block loads its values
+// with float4 loads, formats 8 pixels per thread (branch-free toInt and "%d " words), finds its byte
+// offset by a block scan plus a decoupled look-back over its predecessors' published lengths,
+// assembles its text in LDS at the destination's 16-byte phase and writes it with 16-byte stores.
 // P6 / PFM are fixed-size: grid-stride float4 loops, one dword / float4 store per 4 values.
 // toInt is the reference's double-precision formula exactly: a 256-entry threshold table computed
 // on the host with that very formula (toInt is monotone in x) settles a v_log/v_exp estimate,
@@ -31,7 +31,14 @@ constexpr int kThreads = 256;
 #define SPT_P3_PIX_PER_THREAD 8
 #endif
 constexpr int kPixPerThread = SPT_P3_PIX_PER_THREAD;    // P3: pixels formatted per thread
-constexpr int kPixPerBlock = kThreads * kPixPerThread;  // 2048 (4096² P3: 177 µs at 8, 227 at 4, 193 at 12)
+#ifndef SPT_P3_THREADS
+#define SPT_P3_THREADS 512
+#endif
+// P3 blocks are larger than the others: every block takes one ticket from a single counter (the
+// look-back's order), and a returning atomic on one word saturates near 88 per us
+// (MI355X_MICROARCH.md, dequeue): 8192 blocks of 2048 pixels at 4096^2 cost >= 93 us of tickets.
+constexpr int kP3Threads = SPT_P3_THREADS;
+constexpr int kPixPerBlock = kP3Threads * kPixPerThread;  // 4096 (r03_ab.txt session 13/14)
 static_assert(kPixPerThread % 4 == 0, "whole float4 loads per thread");
 constexpr int kMaxValueText = 12;                        // "-2147483648 "
 
@@ -112,11 +119,12 @@ __device__ __forceinline__ uint32_t put_value(uint8_t* p, int v) {  // "%d " int
 }
 
 __device__ __forceinline__ void load_thr(float* s_thr, const Thresholds& T) {
-  for (int i = threadIdx.x; i < 256; i += kThreads) s_thr[i] = T.t[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_thr[i] = T.t[i];
   __syncthreads();
 }
 
 // Block-wide exclusive scan of one uint32 per thread (wave shuffles + LDS for wave totals).
+template <int kBlockThreads>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t incl = v;
@@ -129,7 +137,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   __syncthreads();
   uint32_t base = 0, all = 0;
 #pragma unroll
-  for (int w = 0; w < kThreads / 64; ++w) {
+  for (int w = 0; w < kBlockThreads / 64; ++w) {
     const uint32_t t = s_wave[w];
     base += w < wave ? t : 0u;
     all += t;
@@ -156,18 +164,18 @@ __device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kP3Threads)
 p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t header_len,
           uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint8_t* __restrict__ out,
           uint64_t cap, uint64_t* __restrict__ total_out) {
   __shared__ float s_thr[256];
-  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint32_t s_wave[kP3Threads / 64];
   __shared__ __attribute__((aligned(16))) uint32_t s_dw[kStageP3 / 4];
   uint8_t* const s_txt = (uint8_t*)s_dw;
   __shared__ uint32_t s_bid;
   __shared__ uint64_t s_prefix;
   if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
-  for (int i = threadIdx.x; i < kStageP3 / 16; i += kThreads)  // the OR-assembled staging starts at 0
+  for (int i = threadIdx.x; i < kStageP3 / 16; i += kP3Threads)  // the OR-assembled staging starts at 0
     ((uint4*)s_dw)[i] = make_uint4(0u, 0u, 0u, 0u);
   load_thr(s_thr, T);  // barrier
   const uint32_t bid = s_bid;
@@ -198,7 +206,7 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   }
   const bool block_nan = __syncthreads_or(nan) != 0;
   uint32_t total;
-  const uint32_t my = block_excl_scan(len, s_wave, &total);
+  const uint32_t my = block_excl_scan<kP3Threads>(len, s_wave, &total);
   if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors per step
     const uint32_t lane = threadIdx.x;
     uint64_t excl = header_len;
@@ -275,13 +283,13 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   if (nb) atomicOr(&s_dw[di], (uint32_t)acc);
   __syncthreads();
   if (dst + total > cap) {  // the host reports the error; write nothing past cap
-    for (uint32_t i = threadIdx.x; i < total; i += kThreads)
+    for (uint32_t i = threadIdx.x; i < total; i += kP3Threads)
       if (dst + i < cap) out[dst + i] = s_txt[phase + i];
     return;
   }
   const uint64_t a0 = (dst + 15u) & ~15ull, a1 = (dst + total) & ~15ull;
   if (a0 >= a1) {
-    for (uint32_t i = threadIdx.x; i < total; i += kThreads) out[dst + i] = s_txt[phase + i];
+    for (uint32_t i = threadIdx.x; i < total; i += kP3Threads) out[dst + i] = s_txt[phase + i];
     return;
   }
   // 16-byte stores: the staging sits at the destination's 16-byte phase, so phase + head is 0 or 16
@@ -291,7 +299,7 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   const uint32_t n_q = (uint32_t)((a1 - a0) >> 4);
   const uint4* s_q = (const uint4*)(s_txt + phase + head);
   uint4* o_q = (uint4*)(out + a0);
-  for (uint32_t i = threadIdx.x; i < n_q; i += kThreads) o_q[i] = s_q[i];
+  for (uint32_t i = threadIdx.x; i < n_q; i += kP3Threads) o_q[i] = s_q[i];
 }
 
 // P6: header (padded to 16 bytes, see header()), then toInt bytes (the int's low byte, as a
@@ -446,7 +454,7 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
     }
     IMG_HIP(hipMemsetAsync(e->status, 0, sizeof(uint64_t) * (nb + 1), stream));
     if (cap >= hd.size()) IMG_HIP(hipMemcpyAsync(out_dev, hd.data(), hd.size(), hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(p3_single, dim3(nb), dim3(kThreads), 0, stream, rgb_dev, n_pix, T,
+    hipLaunchKernelGGL(p3_single, dim3(nb), dim3(kP3Threads), 0, stream, rgb_dev, n_pix, T,
                        (uint64_t)hd.size(), (uint32_t*)(e->status + nb), e->status, out_dev, cap, e->total);
     IMG_HIP(hipGetLastError());
     IMG_HIP(hipMemcpyAsync(e->h_total, e->total, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
