@@ -1393,6 +1393,11 @@ struct spt_context {
   uint32_t* queue = nullptr;
   unsigned long long* stats = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // the launch's statistics words, copied to pinned host memory on the launch's stream after the
+  // finalize (ev2 marks the copy): spt_context_stats() waits for that launch only, never for work
+  // queued behind it on the stream
+  unsigned long long* h_stats = nullptr;
+  hipEvent_t ev2 = nullptr;
   bool pending = false;
   int n_prims = 0;
   KParams last{};
@@ -1615,6 +1620,8 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * kStatWords);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev2);
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_stats, sizeof(unsigned long long) * kStatWords, hipHostMallocDefault);
   if (e != hipSuccess) {
     spt_context_destroy(c);
     return fail(SPT_ERR_OOM, std::string("context alloc: ") + hipGetErrorString(e));
@@ -1638,6 +1645,8 @@ extern "C" spt_status spt_context_destroy(spt_context* c) {
   if (c->stats) (void)hipFree(c->stats);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  if (c->h_stats) (void)hipHostFree(c->h_stats);
   delete c;
   return SPT_OK;
 }
@@ -1702,6 +1711,9 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
     SPT_HIP(hipEventRecord(c->ev0, stream));
     SPT_HIP(hipEventRecord(c->ev1, stream));
+    SPT_HIP(hipMemcpyAsync(c->h_stats, c->stats, sizeof(unsigned long long) * kStatWords,
+                           hipMemcpyDeviceToHost, stream));
+    SPT_HIP(hipEventRecord(c->ev2, stream));
     c->pending = true;
     return SPT_OK;
   }
@@ -1883,6 +1895,9 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                      (const unsigned long long*)c->accum, rgb_dev, n);
 #endif
   SPT_HIP(hipGetLastError());
+  SPT_HIP(hipMemcpyAsync(c->h_stats, c->stats, sizeof(unsigned long long) * kStatWords,
+                         hipMemcpyDeviceToHost, stream));
+  SPT_HIP(hipEventRecord(c->ev2, stream));
   c->pending = true;
   return SPT_OK;
 }
@@ -1890,9 +1905,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   if (!c || !out) return fail(SPT_ERR_INVALID_ARG, "null argument");
   SPT_HIP(hipSetDevice(c->device));
-  SPT_HIP(hipEventSynchronize(c->ev1));
-  static thread_local unsigned long long h[kStatWords];
-  SPT_HIP(hipMemcpy(h, c->stats, sizeof h, hipMemcpyDeviceToHost));
+  SPT_HIP(hipEventSynchronize(c->ev2));
+  const unsigned long long* h = c->h_stats;
 #ifdef SPT_WAVE_TIMES
   std::fprintf(stderr, "SPT_WAVE_TIMES sum=%llu sumsq=%llu first=%llu last=%llu iters=%llu maxiters=%llu "
                "sumstart16=%llu sumend16=%llu smid=%llu\n",
