@@ -2,7 +2,7 @@
 # Round-3 measurement session on the GPU box (in-tree build): GPU tests, the C3 rocprofv3 session
 # (kernel trace + separate PMC passes, scripts/profile.sh), instruction-class PMC passes for C3 and
 # C5, and the bench lines of every config (C2-C5, with their CPU baselines).
-#   STEPS=(pytest profile classes bench) selects parts; each GPU step has its own time limit and the
+#   PARTS="pytest smoke rehearsal profile classes bench" selects parts; each GPU step has its own time limit and the
 #   script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -14,6 +14,13 @@ if has pytest; then
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest -m gpu exit $rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has smoke; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+  rc=$?; echo "smoke exit $rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has rehearsal; then  # the N>1 bench path on the one GPU (gloo gather; RCCL needs one GPU per rank)
+  RANKS="${RANKS:-2 4}" bash scripts/rehearsal_r02.sh || exit $?
 fi
 if has profile; then
   bash scripts/profile.sh r03 || exit $?
