@@ -281,6 +281,9 @@ def main() -> None:
                     help="N > 1 over nccl: the library's gather (spt_comm: grouped ncclSend/ncclRecv "
                          "+ de-interleave kernel) or torch.distributed.gather of the shards (RCCL) "
                          "with the de-interleave as torch indexing on rank 0")
+    ap.add_argument("--frames-in-flight", type=int, choices=[1, 2], default=2,
+                    help="2: consecutive frames render on two streams, so a frame's launch fills the "
+                         "CU slots the previous frame's tail frees (1: one stream, frame after frame)")
     ap.add_argument("--init-timeout", type=float, default=300.0,
                     help="seconds allowed for the RCCL / process-group set-up; past it the rank "
                          "prints an error and exits with status 3 (no retry)")
@@ -346,9 +349,18 @@ def main() -> None:
     rens = [spt.Renderer(local), spt.Renderer(local)]
     for r_ in rens:
         r_.reserve(len(prims), params)
-    stream = torch.cuda.current_stream()
-    shard = torch.zeros((max_rows, w, 3), dtype=torch.float32, device="cuda")
-    full = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
+    # Frames in flight: frame k renders into buffer k % nfly on stream k % nfly; the gathers (N > 1)
+    # run in frame order on one stream behind an event of their render, and a frame buffer is not
+    # rendered into again before its previous gather has read it.
+    nfly = args.frames_in_flight
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nfly - 1)]
+    stream = streams[0]
+    comm_stream = torch.cuda.Stream() if (world > 1 and nfly > 1) else stream
+    shards = [torch.zeros((max_rows, w, 3), dtype=torch.float32, device="cuda") for _ in range(nfly)]
+    fulls = ([torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") for _ in range(nfly)]
+             if rank == 0 else [None] * nfly)
+    shard, full = shards[0], fulls[0]
+    gather_done = [None] * nfly
     comm = None
     use_torch_gather = world > 1 and backend == "nccl" and args.gather == "torch"
     # torch.distributed.gather into rank 0's pre-allocated slots, de-interleaved on the device
@@ -404,20 +416,34 @@ def main() -> None:
     def step():
         k = n_step[0]
         n_step[0] += 1
-        rens[k % 2].render_async(prims, cam, params, shard.data_ptr(), stream.cuda_stream)
+        i = k % nfly
+        s_ = streams[i]
+        if gather_done[i] is not None:  # buffer i's previous gather must have read it
+            s_.wait_event(gather_done[i])
+        rens[k % 2].render_async(prims, cam, params, shards[i].data_ptr(), s_.cuda_stream)
         if k > 0:  # the previous step's statistics (its context's last launch)
             kstats.append(rens[(k - 1) % 2].stats())
-        if comm is not None:  # one RCCL gather to rank 0, on the render's stream
-            comm.gather(params, shard.data_ptr(), full.data_ptr() if rank == 0 else 0,
-                        stream.cuda_stream)
-        elif use_torch_gather:  # torch.distributed.gather over RCCL, de-interleave on rank 0
-            sd.gather_rows(shard, rows_of, full, gather_list=slots)
+        if comm is not None or use_torch_gather:
+            ev = torch.cuda.Event()
+            ev.record(s_)
+            comm_stream.wait_event(ev)
+            if comm is not None:  # one RCCL gather to rank 0
+                comm.gather(params, shards[i].data_ptr(), fulls[i].data_ptr() if rank == 0 else 0,
+                            comm_stream.cuda_stream)
+            else:  # torch.distributed.gather over RCCL, de-interleave on rank 0
+                with torch.cuda.stream(comm_stream):
+                    sd.gather_rows(shards[i], rows_of, fulls[i], gather_list=slots)
+            gd = torch.cuda.Event()
+            gd.record(comm_stream)
+            gather_done[i] = gd
         elif world > 1:
-            host = sd.gather_rows(shard.cpu(), rows_of, full.cpu() if rank == 0 else None)
-            if rank == 0:
-                full.copy_(host)
+            with torch.cuda.stream(s_):
+                host = sd.gather_rows(shards[i].cpu(), rows_of, fulls[i].cpu() if rank == 0 else None)
+                if rank == 0:
+                    fulls[i].copy_(host)
         else:
-            full.copy_(shard[: len(my_rows)])
+            with torch.cuda.stream(s_):
+                fulls[i].copy_(shards[i][: len(my_rows)])
 
     watchdog.cancel()  # set-up done (the first gather below has its own collective timeout)
     def drain():  # the last queued step's statistics
@@ -443,6 +469,17 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     drain()
     assert len(kstats) == args.steps, (len(kstats), args.steps)
+    last = (args.steps - 1) % nfly
+    shard, full = shards[last], fulls[last]
+    # The roofline's kernel time: with two frames in flight a launch's HIP-event span also covers
+    # the neighbouring frame's overlap, so the per-launch time is measured on 3 launches run one at
+    # a time after the timed region (the same kernel and work; rocprofv3 sees them as well).
+    kms_flight = float(np.mean([s["kernel_ms"] for s in kstats]))
+    iso = []
+    for _ in range(3 if nfly > 1 else 0):
+        rens[0].render_async(prims, cam, params, shards[0].data_ptr(), streams[0].cuda_stream)
+        iso.append(rens[0].stats())
+    torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device="cuda" if backend == "nccl" else "cpu")
@@ -451,9 +488,10 @@ def main() -> None:
 
     samples_per_step = w * h * spp  # all ranks together (each rank renders its rows at spp)
     value = samples_per_step * args.steps / elapsed / 1e6
-    kms = np.array([s["kernel_ms"] for s in kstats])
-    flop = np.array([s["flop"] for s in kstats])
-    flop_x = np.array([s["flop_executed"] for s in kstats])
+    kst = iso if iso else kstats
+    kms = np.array([s["kernel_ms"] for s in kst])
+    flop = np.array([s["flop"] for s in kst])
+    flop_x = np.array([s["flop_executed"] for s in kst])
     achieved = float((flop / (kms * 1e-3)).mean() / 1e12)
     achieved_x = float((flop_x / (kms * 1e-3)).mean() / 1e12)
     s0 = kstats[-1]
@@ -527,6 +565,7 @@ def main() -> None:
                                                    if scaling == "weak" and world > 1 else ""),
                        "width": w, "height": h, "spp": spp,
                        "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",
+                       "frames_in_flight": nfly,
                        "parallelism": (f"row-tile x{world} (tile 8 rows, cyclic) + one gather to rank 0 "
                                        f"({('RCCL, ' + ('torch.distributed.gather' if use_torch_gather else 'spt_comm grouped send/recv')) if backend == 'nccl' else backend})")
                                       if world > 1 else "1 GPU"},
@@ -548,6 +587,13 @@ def main() -> None:
                          "valu_pmc": pmc or None,
                          "kernel": "spt::render_kernel",
                          "kernel_ms": round(float(kms.mean()), 3),
+                         "kernel_ms_source": ("3 launches one at a time after the timed region"
+                                              if iso else "the timed launches"),
+                         # frames in flight: the same FLOP over the GPU time per frame of the
+                         # timed run (elapsed / steps, the neighbouring frame filling each tail)
+                         "frac_pipelined": round(float(flop.mean()) / (elapsed / args.steps)
+                                                 / 1e12 / PEAK_FP32_TFLOPS, 4),
+                         "kernel_ms_in_flight": round(kms_flight, 3),
                          "flop_per_launch": float(flop.mean()),
                          "flop_per_sample": round(float(flop.mean()) / my_samples, 1)},
             "paths": {"vertices_per_sample": round(s0["vertices"] / my_samples, 4),
