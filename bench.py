@@ -281,9 +281,9 @@ def main() -> None:
                     help="N > 1 over nccl: the library's gather (spt_comm: grouped ncclSend/ncclRecv "
                          "+ de-interleave kernel) or torch.distributed.gather of the shards (RCCL) "
                          "with the de-interleave as torch indexing on rank 0")
-    ap.add_argument("--frames-in-flight", type=int, choices=[1, 2], default=2,
-                    help="2: consecutive frames render on two streams, so a frame's launch fills the "
-                         "CU slots the previous frame's tail frees (1: one stream, frame after frame)")
+    ap.add_argument("--frames-in-flight", type=int, choices=[1, 2, 3, 4], default=2,
+                    help="N > 1: consecutive frames render on N streams, so a frame's launch fills the "
+                         "CU slots the previous frames' tails free (1: one stream, frame after frame)")
     ap.add_argument("--init-timeout", type=float, default=300.0,
                     help="seconds allowed for the RCCL / process-group set-up; past it the rank "
                          "prints an error and exits with status 3 (no retry)")
@@ -344,15 +344,19 @@ def main() -> None:
     assert np.array_equal(spt.shard_rows(params), my_rows)
     max_rows = sd.max_rows(rows_of)
 
-    # Two render contexts used in turn: a step's statistics (kernel time, event counts) are read
-    # after the NEXT step is queued, so reading them never stalls the stream between steps.
-    rens = [spt.Renderer(local), spt.Renderer(local)]
-    for r_ in rens:
-        r_.reserve(len(prims), params)
     # Frames in flight: frame k renders into buffer k % nfly on stream k % nfly; the gathers (N > 1)
     # run in frame order on one stream behind an event of their render, and a frame buffer is not
     # rendered into again before its previous gather has read it.
     nfly = args.frames_in_flight
+    # Render contexts used in turn, one per frame in flight (two at least): a step's statistics
+    # (kernel time, event counts) are read `lag` steps later, after the steps in flight behind it
+    # are queued, so reading them never stalls the streams between steps. Context k % n_ctx always
+    # runs on the same stream (n_ctx == nfly) or on the one stream (nfly == 1).
+    n_ctx = max(2, nfly)
+    lag = max(1, nfly - 1)
+    rens = [spt.Renderer(local) for _ in range(n_ctx)]
+    for r_ in rens:
+        r_.reserve(len(prims), params)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nfly - 1)]
     stream = streams[0]
     comm_stream = torch.cuda.Stream() if (world > 1 and nfly > 1) else stream
@@ -420,9 +424,9 @@ def main() -> None:
         s_ = streams[i]
         if gather_done[i] is not None:  # buffer i's previous gather must have read it
             s_.wait_event(gather_done[i])
-        rens[k % 2].render_async(prims, cam, params, shards[i].data_ptr(), s_.cuda_stream)
-        if k > 0:  # the previous step's statistics (its context's last launch)
-            kstats.append(rens[(k - 1) % 2].stats())
+        rens[k % n_ctx].render_async(prims, cam, params, shards[i].data_ptr(), s_.cuda_stream)
+        if k >= lag:  # the statistics of the step `lag` back (its context's last launch)
+            kstats.append(rens[(k - lag) % n_ctx].stats())
         if comm is not None or use_torch_gather:
             ev = torch.cuda.Event()
             ev.record(s_)
@@ -446,9 +450,9 @@ def main() -> None:
                 fulls[i].copy_(shards[i][: len(my_rows)])
 
     watchdog.cancel()  # set-up done (the first gather below has its own collective timeout)
-    def drain():  # the last queued step's statistics
-        if n_step[0] > 0:
-            kstats.append(rens[(n_step[0] - 1) % 2].stats())
+    def drain():  # the statistics of the last `lag` queued steps
+        for j in range(max(0, n_step[0] - lag), n_step[0]):
+            kstats.append(rens[j % n_ctx].stats())
         n_step[0] = 0
 
     # every context's first launch allocates its unit slots: warm both up, whatever --warmup says
