@@ -3,10 +3,11 @@
 //
 // The reference writes `fprintf(f, "%d %d %d ", toInt(r), toInt(g), toInt(b))` per pixel: ASCII
 // P3, 6-12 bytes per pixel, ~200 MB of text at 4096². Here the framebuffer never leaves HBM until
-// the bytes are final, in ONE HBM-bound pass (p3_single): each 4096-pixel block loads its values
-// with float4 loads, formats 8 pixels per thread (branch-free toInt and "%d " words), finds its byte
-// offset by a block scan plus a decoupled look-back over its predecessors' published lengths,
-// assembles its text in LDS at the destination's 16-byte phase and writes it with 16-byte stores.
+// the bytes are final. P3 takes four short HBM-bound passes split at the toInt bytes (p6_write ->
+// p3_lengths -> p3_offsets -> p3_text, below): the bytes, each 8192-value text block's length,
+// the blocks' byte offsets, then the "%d " text assembled in LDS at the destination's 16-byte phase
+// and written with 16-byte stores. (Rounds 1-3 used one pass with a decoupled look-back; at 4096^2
+// it took 155.6 us against 132-136 us for the passes, profiles/r03_encoder.txt.)
 // P6 / PFM are fixed-size: grid-stride float4 loops, one dword / float4 store per 4 values.
 // toInt is the reference's double-precision formula exactly: a 256-entry threshold table computed
 // on the host with that very formula (toInt is monotone in x) settles a v_log/v_exp estimate,
@@ -27,19 +28,6 @@
 namespace spt_img {
 
 constexpr int kThreads = 256;
-#ifndef SPT_P3_PIX_PER_THREAD
-#define SPT_P3_PIX_PER_THREAD 8
-#endif
-constexpr int kPixPerThread = SPT_P3_PIX_PER_THREAD;    // P3: pixels formatted per thread
-#ifndef SPT_P3_THREADS
-#define SPT_P3_THREADS 512
-#endif
-// P3 blocks are larger than the others: every block takes one ticket from a single counter (the
-// look-back's order), and a returning atomic on one word saturates near 88 per us
-// (MI355X_MICROARCH.md, dequeue): 8192 blocks of 2048 pixels at 4096^2 cost >= 93 us of tickets.
-constexpr int kP3Threads = SPT_P3_THREADS;
-constexpr int kPixPerBlock = kP3Threads * kPixPerThread;  // 4096 (r03_ab.txt session 13/14)
-static_assert(kPixPerThread % 4 == 0, "whole float4 loads per thread");
 constexpr int kMaxValueText = 12;                        // "-2147483648 "
 
 struct Thresholds { float t[256]; };  // t[k] = smallest x with toInt(x) >= k; t[0] = -inf
@@ -146,120 +134,161 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   return base + incl - v;
 }
 
-// ---- single-pass P3: decoupled look-back (Merrill & Garland 2016) over kPixPerBlock-pixel blocks.
-// Blocks take a ticket at start, so every predecessor of a block is resident or finished and the
-// look-back always makes progress. status[b] = flag << 62 | value: flag 1 = the block's own
-// aggregate, 2 = its inclusive prefix (header included). Agent-scope atomics on the status words
-// keep the hand-off coherent across the XCDs' L2s.
-constexpr int kStageP3 = kPixPerBlock * 3 * 4 + 32;  // every value <= "255 ": 24 KB + the phase
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+// ---- P3 in passes (round 3). The round-1/2 single pass serialised each block's phases (ticket,
+// loads, toInt, scan, look-back, staging, stores) and held 48 KB of LDS per 512-thread block (3
+// blocks per CU). Split at the toInt bytes instead:
+//   p6_write:   toInt of every value as one byte (the P6 kernel itself: coalesced float4 loads, dword
+//               stores), and the encode's epoch in a NaN word if any value is NaN;
+//   p3_lengths: each 8192-value text block's length from its bytes;
+//   p3_offsets: one block scans the text-block lengths (header first) into byte offsets;
+//   p3_text:    each 512-thread block formats 16 contiguous digits per thread ("%d " words), scans
+//               the thread lengths, assembles its text in LDS at the destination's 16-byte phase
+//               and writes it with 16-byte stores.
+// HBM traffic per value: 4 B read + 1 B written, 1 B read, 1 B read + 2-4 B written, with no
+// cross-block dependency inside a pass. (An image with a NaN, "-2147483648 ", takes an exact slow
+// path in the last two passes: toInt again from the floats, byte stores.)
+constexpr int kTxtThreads = 512, kTxtVals = 16, kTxtBlockVals = kTxtThreads * kTxtVals;  // 8192
+constexpr int kStageTxt = kTxtBlockVals * 4 + 32;  // every value <= "255 ", + the 16-byte phase
 
-// Relaxed agent-scope atomics: the status word is the only datum that crosses blocks (no other
-// memory is read after it), so no acquire/release fences — at agent scope those cost an L1
-// invalidate / an L2 write-back of the block's dirty text per step (MI355X_MICROARCH.md).
-__device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Pass 1 is the P6 kernel itself (p6_write with a NaN word: the toInt bytes, 1 B per value, and the
+// encode's epoch stored in *nan_word if any value is NaN). Pass 2, here: each 8192-value text
+// block's length from its bytes (one 16-byte load per thread, block reduce). With a NaN in the
+// image every block takes the exact slow path (toInt again from the floats).
+// (Round 3: computing the lengths inside pass 1 -- one block per text block, persistent blocks, or
+// the P6 loop with a per-wave atomic -- ran at 67-77 us at 4096^2, against 42 us for the P6 loop
+// alone plus ~10 us for this pass.)
+__device__ __forceinline__ bool nan_seen(const uint32_t* nan_word, uint32_t epoch) {
+  return __hip_atomic_load(nan_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
 }
-__device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint32_t digit_len(uint32_t b) {  // "%d " of a toInt byte
+  return 2u + (uint32_t)(b >= 10u) + (uint32_t)(b >= 100u);
 }
 
-__global__ void __launch_bounds__(kP3Threads)
-p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t header_len,
-          uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint8_t* __restrict__ out,
-          uint64_t cap, uint64_t* __restrict__ total_out) {
+__global__ void __launch_bounds__(kTxtThreads)
+p3_lengths(const uint4* __restrict__ digits, const float* __restrict__ rgb, uint32_t nv, Thresholds T,
+           const uint32_t* __restrict__ nan_word, uint32_t epoch, uint32_t* __restrict__ blen) {
   __shared__ float s_thr[256];
-  __shared__ uint32_t s_wave[kP3Threads / 64];
-  __shared__ __attribute__((aligned(16))) uint32_t s_dw[kStageP3 / 4];
-  uint8_t* const s_txt = (uint8_t*)s_dw;
-  __shared__ uint32_t s_bid;
-  __shared__ uint64_t s_prefix;
-  if (threadIdx.x == 0) s_bid = atomicAdd(ticket, 1u);
-  for (int i = threadIdx.x; i < kStageP3 / 16; i += kP3Threads)  // the OR-assembled staging starts at 0
-    ((uint4*)s_dw)[i] = make_uint4(0u, 0u, 0u, 0u);
-  load_thr(s_thr, T);  // barrier
-  const uint32_t bid = s_bid;
-  const uint64_t b0 = (uint64_t)bid * kPixPerBlock * 3, nv = (uint64_t)n_pix * 3;
-  const uint64_t v0 = b0 + (uint64_t)threadIdx.x * kPixPerThread * 3;
-  float x[kPixPerThread * 3];
-  if (v0 + kPixPerThread * 3 <= nv) {  // 12 B per pixel, contiguous per thread: float4 loads
-    const float4* q = (const float4*)(rgb + v0);
-#pragma unroll
-    for (int k = 0; k < kPixPerThread * 3 / 4; ++k) {
-      const float4 f = q[k];
-      x[4 * k] = f.x; x[4 * k + 1] = f.y; x[4 * k + 2] = f.z; x[4 * k + 3] = f.w;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < kPixPerThread * 3; ++i) x[i] = v0 + i < nv ? rgb[v0 + i] : 0.0f;
-  }
-  // toInt values; -1 marks a slot past the image's end (no text), INT_MIN a NaN (12 bytes)
-  int vals[kPixPerThread * 3];
+  __shared__ uint32_t s_red[kTxtThreads / 64];
+  const uint32_t v0 = blockIdx.x * (uint32_t)kTxtBlockVals + threadIdx.x * (uint32_t)kTxtVals;
+  const uint32_t n_in = v0 < nv ? min((uint32_t)kTxtVals, nv - v0) : 0u;  // nv < 2^32
   uint32_t len = 0;
-  bool nan = false;
+  if (nan_seen(nan_word, epoch)) {  // grid-uniform
+    load_thr(s_thr, T);
+#pragma unroll 1
+    for (uint32_t i = 0; i < n_in; ++i) len += text_len(dev_toInt_bf(s_thr, rgb[v0 + i]));
+  } else {
+    uint4 q = make_uint4(0u, 0u, 0u, 0u);
+    if (n_in) q = digits[v0 >> 4];  // the digits are padded to whole 16-byte groups
+    const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-  for (int i = 0; i < kPixPerThread * 3; ++i) {
-    const int v = dev_toInt_bf(s_thr, x[i]);
-    vals[i] = v0 + i < nv ? v : -1;
-    nan |= vals[i] == (int)0x80000000;
-    len += text_len(vals[i]);
+    for (int i = 0; i < kTxtVals; ++i)
+      len += (uint32_t)i < n_in ? digit_len((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu) : 0u;
   }
-  const bool block_nan = __syncthreads_or(nan) != 0;
-  uint32_t total;
-  const uint32_t my = block_excl_scan<kP3Threads>(len, s_wave, &total);
-  if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 predecessors per step
-    const uint32_t lane = threadIdx.x;
-    uint64_t excl = header_len;
-    if (bid == 0) {
-      if (lane == 0) status_store(status, kFlagInc | (header_len + total));
-    } else {
-      if (lane == 0) status_store(status + bid, kFlagAgg | total);
-      excl = 0;
-      int64_t top = (int64_t)bid - 1;  // window [top - 63, top], lane l reads top - l
-      uint32_t spins = 0;
-      while (top >= 0) {
-        const int64_t j = top - (int64_t)lane;
-        const uint64_t st = j >= 0 ? status_load(status + j) : kFlagInc;  // "before block 0" = 0
-        const uint32_t flag = (uint32_t)(st >> 62);
-        const uint64_t ready = __ballot(flag != 0), inc = __ballot(flag == 2);
-        const uint32_t n_inc = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive
-        const uint64_t need = n_inc == 64u ? ~0ull : ((2ull << n_inc) - 1);   // lanes 0..n_inc
-        if ((ready & need) != need) {  // a predecessor in the window has not published yet
-          if (++spins > (1u << 24)) {  // cannot happen (tickets order the blocks); never hang
-            if (lane == 0) *total_out = ~0ull;
-            break;
-          }
-          continue;
-        }
-        uint64_t v = lane <= n_inc && j >= 0 ? (st & kValMask) : 0;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-        excl += v;
-        if (n_inc < 64u) break;
-        top -= 64;
-      }
-      if (lane == 0) status_store(status + bid, kFlagInc | (excl + total));
-    }
-    if (lane == 0) {
-      s_prefix = excl;
-      if (bid == gridDim.x - 1) *total_out = excl + total;
-    }
-  }
+  for (int off = 32; off >= 1; off >>= 1) len += __shfl_xor(len, off, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = len;
   __syncthreads();
-  const uint64_t dst = s_prefix;
-  if (block_nan || total + 32 > (uint32_t)kStageP3) {  // a NaN (12-byte text): direct byte stores
-    uint64_t q = dst + my;
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
 #pragma unroll
-    for (int i = 0; i < kPixPerThread * 3; ++i) {
-      if (vals[i] == -1) break;
-      uint8_t b[12];
-      const uint32_t n = put_value(b, vals[i]);
-      for (uint32_t k = 0; k < n; ++k, ++q)
-        if (q < cap) out[q] = b[k];
+    for (int w = 0; w < kTxtThreads / 64; ++w) t += s_red[w];
+    blen[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of the text-block lengths into byte offsets (header first); *total = the length.
+// Super-rounds of 8192 entries: each thread loads its 8 contiguous entries at once (one memory
+// latency), one block scan of the thread sums, then the running carry.
+constexpr int kScanThreads = 1024, kScanPer = 8;
+__global__ void __launch_bounds__(kScanThreads)
+p3_offsets(const uint32_t* __restrict__ blen, uint32_t nb, uint64_t header_len,
+           uint64_t* __restrict__ offs, uint64_t* __restrict__ total) {
+  __shared__ uint64_t s_wave[2][kScanThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t carry = header_len;
+  int par = 0;
+  for (uint32_t r0 = 0; r0 < nb; r0 += kScanThreads * kScanPer, par ^= 1) {
+    const uint32_t b0 = r0 + threadIdx.x * kScanPer;
+    uint32_t v[kScanPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) v[i] = b0 + i < nb ? blen[b0 + i] : 0u;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) sum += v[i];
+    uint64_t incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t u = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += u;
     }
+    if (lane == 63) s_wave[par][wave] = incl;  // (double-buffered: one barrier per round)
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+      const uint64_t t = s_wave[par][w];
+      before += w < wave ? t : 0ull;
+      all += t;
+    }
+    uint64_t run = carry + before + incl - sum;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+      if (b0 + i < nb) offs[b0 + i] = run;
+      run += v[i];
+    }
+    carry += all;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// A text block holding a NaN (12-byte "-2147483648 "): toInt again from the floats (twice: lengths,
+// then bytes; rolled loops keep the registers of the common path), byte stores.
+__device__ __forceinline__ void p3_text_nan(const float* __restrict__ rgb, uint32_t nv, const float* s_thr,
+                                            uint64_t dst, uint8_t* __restrict__ out, uint64_t cap,
+                                            uint32_t* s_wave) {
+  const uint32_t v0 = blockIdx.x * (uint32_t)kTxtBlockVals + threadIdx.x * (uint32_t)kTxtVals;
+  const uint32_t n_in = v0 < nv ? min((uint32_t)kTxtVals, nv - v0) : 0u;
+  uint32_t len = 0;
+#pragma unroll 1
+  for (uint32_t i = 0; i < n_in; ++i) len += text_len(dev_toInt_bf(s_thr, rgb[v0 + i]));
+  uint32_t total;
+  uint64_t q = dst + block_excl_scan<kTxtThreads>(len, s_wave, &total);
+#pragma unroll 1
+  for (uint32_t i = 0; i < n_in; ++i) {
+    uint8_t b[12];
+    const uint32_t n = put_value(b, dev_toInt_bf(s_thr, rgb[v0 + i]));
+    for (uint32_t k = 0; k < n; ++k, ++q)
+      if (q < cap) out[q] = b[k];
+  }
+}
+
+__global__ void __launch_bounds__(kTxtThreads) __attribute__((amdgpu_waves_per_eu(8)))  // 4 blocks per CU
+p3_text(const uint4* __restrict__ digits, const float* __restrict__ rgb, uint32_t nv, Thresholds T,
+        const uint32_t* __restrict__ nan_word, uint32_t epoch, const uint64_t* __restrict__ offs,
+        uint8_t* __restrict__ out, uint64_t cap) {
+  __shared__ uint32_t s_wave[kTxtThreads / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_dw[kStageTxt / 4];
+  uint8_t* const s_txt = (uint8_t*)s_dw;
+  const uint64_t dst = offs[blockIdx.x];
+  if (nan_seen(nan_word, epoch)) {  // grid-uniform
+    load_thr((float*)s_dw, T);
+    p3_text_nan(rgb, nv, (const float*)s_dw, dst, out, cap, s_wave);
     return;
   }
-  // Stage the block's text at the destination's 16-byte phase. Each value's text (2-4 bytes) is
+  const uint32_t v0 = blockIdx.x * (uint32_t)kTxtBlockVals + threadIdx.x * (uint32_t)kTxtVals;
+  const uint32_t n_in = v0 < nv ? min((uint32_t)kTxtVals, nv - v0) : 0u;  // values here (nv < 2^32)
+  uint4 q = make_uint4(0u, 0u, 0u, 0u);
+  if (n_in) q = digits[v0 >> 4];  // the digits are padded to whole 16-byte groups
+  const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+  uint32_t len = 0;
+#pragma unroll
+  for (int i = 0; i < kTxtVals; ++i)
+    len += (uint32_t)i < n_in ? digit_len((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu) : 0u;
+  for (int i = threadIdx.x; i < kStageTxt / 16; i += kTxtThreads)  // OR-assembled staging starts at 0
+    ((uint4*)s_dw)[i] = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t total;
+  const uint32_t my = block_excl_scan<kTxtThreads>(len, s_wave, &total);  // (its barrier orders the zeroing)
+  // Stage the text at the destination's 16-byte phase. Each value's "%d " word (2-4 bytes) is
   // appended to a 64-bit accumulator at the thread's byte offset and its low dword ORed into the
   // zeroed staging after every value (ds_or: a thread's first and last dword are shared with its
   // neighbours; re-ORing a growing dword is idempotent); the dword index advances once 32 bits are
@@ -269,11 +298,11 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   uint32_t di = o >> 2, nb = (o & 3u) * 8u;
   uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < kPixPerThread * 3; ++i) {
+  for (int i = 0; i < kTxtVals; ++i) {
     uint32_t n;
-    const uint32_t wv = text_word(max(vals[i], 0), n);
+    const uint32_t wv = text_word((int)((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu), n);
     acc |= (uint64_t)wv << nb;
-    nb += vals[i] < 0 ? 0u : 8u * n;  // -1: past the image's end
+    nb += (uint32_t)i < n_in ? 8u * n : 0u;
     atomicOr(&s_dw[di], (uint32_t)acc);
     const uint32_t full = nb >> 5;  // 0 or 1
     acc = full ? acc >> 32 : acc;
@@ -283,40 +312,45 @@ p3_single(const float* __restrict__ rgb, uint32_t n_pix, Thresholds T, uint64_t 
   if (nb) atomicOr(&s_dw[di], (uint32_t)acc);
   __syncthreads();
   if (dst + total > cap) {  // the host reports the error; write nothing past cap
-    for (uint32_t i = threadIdx.x; i < total; i += kP3Threads)
+    for (uint32_t i = threadIdx.x; i < total; i += kTxtThreads)
       if (dst + i < cap) out[dst + i] = s_txt[phase + i];
     return;
   }
   const uint64_t a0 = (dst + 15u) & ~15ull, a1 = (dst + total) & ~15ull;
   if (a0 >= a1) {
-    for (uint32_t i = threadIdx.x; i < total; i += kP3Threads) out[dst + i] = s_txt[phase + i];
+    for (uint32_t i = threadIdx.x; i < total; i += kTxtThreads) out[dst + i] = s_txt[phase + i];
     return;
   }
-  // 16-byte stores: the staging sits at the destination's 16-byte phase, so phase + head is 0 or 16
   const uint32_t head = (uint32_t)(a0 - dst), tail = (uint32_t)(dst + total - a1);
   if (threadIdx.x < head) out[dst + threadIdx.x] = s_txt[phase + threadIdx.x];
   if (threadIdx.x < tail) out[a1 + threadIdx.x] = s_txt[phase + (uint32_t)(a1 - dst) + threadIdx.x];
   const uint32_t n_q = (uint32_t)((a1 - a0) >> 4);
   const uint4* s_q = (const uint4*)(s_txt + phase + head);
   uint4* o_q = (uint4*)(out + a0);
-  for (uint32_t i = threadIdx.x; i < n_q; i += kP3Threads) o_q[i] = s_q[i];
+  for (uint32_t i = threadIdx.x; i < n_q; i += kTxtThreads) o_q[i] = s_q[i];
 }
 
 // P6: header (padded to 16 bytes, see header()), then toInt bytes (the int's low byte, as a
 // byte-writing port would store). Grid-stride over float4 chunks: 4 values -> one dword store.
 __global__ void __launch_bounds__(kThreads)
-p6_write(const float4* __restrict__ rgb, uint32_t n_vals, Thresholds T, uint32_t* __restrict__ out) {
+p6_write(const float4* __restrict__ rgb, uint32_t n_vals, Thresholds T, uint32_t* __restrict__ out,
+         uint32_t* __restrict__ nan_word, uint32_t epoch) {  // nan_word: P3's pass 1 (else null)
   __shared__ float s_thr[256];
   load_thr(s_thr, T);
   const uint32_t n4 = n_vals / 4;
   for (uint32_t c = blockIdx.x * kThreads + threadIdx.x; c < n4; c += gridDim.x * kThreads) {
     const float4 v = rgb[c];
-    out[c] = (uint32_t)(uint8_t)dev_toInt(s_thr, v.x) | (uint32_t)(uint8_t)dev_toInt(s_thr, v.y) << 8 |
-             (uint32_t)(uint8_t)dev_toInt(s_thr, v.z) << 16 | (uint32_t)(uint8_t)dev_toInt(s_thr, v.w) << 24;
+    const int a = dev_toInt(s_thr, v.x), b = dev_toInt(s_thr, v.y), d = dev_toInt(s_thr, v.z),
+              e = dev_toInt(s_thr, v.w);
+    out[c] = (uint32_t)(uint8_t)a | (uint32_t)(uint8_t)b << 8 | (uint32_t)(uint8_t)d << 16 |
+             (uint32_t)(uint8_t)e << 24;
+    if (nan_word && (a | b | d | e) < 0) *nan_word = epoch;  // toInt >= 0 except int(NaN) = INT_MIN
   }
   if (blockIdx.x == 0 && threadIdx.x < (n_vals & 3u)) {  // ragged tail (n_vals % 4 values)
     const uint32_t i = n4 * 4 + threadIdx.x;
-    ((uint8_t*)out)[i] = (uint8_t)dev_toInt(s_thr, ((const float*)rgb)[i]);
+    const int a = dev_toInt(s_thr, ((const float*)rgb)[i]);
+    ((uint8_t*)out)[i] = (uint8_t)a;
+    if (nan_word && a < 0) *nan_word = epoch;
   }
 }
 
@@ -374,8 +408,9 @@ using namespace spt_img;
 
 struct spt_encoder {
   int device = 0;
-  uint64_t* status = nullptr;    // single-pass P3 look-back words + ticket
-  uint32_t cap_blocks = 0;
+  uint8_t* scratch = nullptr;    // two-pass P3: offsets, block lengths, NaN word, digits
+  size_t scratch_cap = 0;        // bytes
+  uint32_t epoch = 0;            // P3 encodes so far: the NaN word holds the epoch of the last NaN
   uint64_t* total = nullptr;     // device word: encoded length
   uint64_t* h_total = nullptr;   // pinned mirror
 };
@@ -423,7 +458,7 @@ extern "C" spt_status spt_encoder_create(int32_t device, spt_encoder** out) {
 extern "C" spt_status spt_encoder_destroy(spt_encoder* e) {
   if (!e) return SPT_OK;
   (void)hipSetDevice(e->device);
-  if (e->status) (void)hipFree(e->status);
+  if (e->scratch) (void)hipFree(e->scratch);
   if (e->total) (void)hipFree(e->total);
   if (e->h_total) (void)hipHostFree(e->h_total);
   delete e;
@@ -444,18 +479,42 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
   const Thresholds& T = thresholds();
   uint64_t len;
   if (format == SPT_IMAGE_P3) {
-    const uint32_t nb = (n_pix + kPixPerBlock - 1) / kPixPerBlock;
-    if (nb + 1 > e->cap_blocks) {  // status words [0, nb) + the ticket
-      if (e->status) IMG_HIP(hipFree(e->status));
-      e->status = nullptr;
-      e->cap_blocks = 0;
-      IMG_HIP(hipMalloc(&e->status, sizeof(uint64_t) * (nb + 1)));
-      e->cap_blocks = nb + 1;
-    }
-    IMG_HIP(hipMemsetAsync(e->status, 0, sizeof(uint64_t) * (nb + 1), stream));
     if (cap >= hd.size()) IMG_HIP(hipMemcpyAsync(out_dev, hd.data(), hd.size(), hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(p3_single, dim3(nb), dim3(kP3Threads), 0, stream, rgb_dev, n_pix, T,
-                       (uint64_t)hd.size(), (uint32_t*)(e->status + nb), e->status, out_dev, cap, e->total);
+    // two passes around the toInt bytes: p6_write (+ NaN epoch) -> p3_lengths -> p3_offsets ->
+    // p3_text, all on the stream
+    const uint32_t nv = n_pix * 3;
+    const uint32_t nbt = (uint32_t)(((uint64_t)nv + kTxtBlockVals - 1) / kTxtBlockVals);
+    const size_t off_b = 0, len_b = off_b + 8ull * nbt, nan_b = len_b + 4ull * nbt;
+    const size_t dig_b = (nan_b + 4 + 15) & ~size_t(15);
+    const size_t need = dig_b + (((size_t)nv + 15) & ~size_t(15));
+    if (need > e->scratch_cap) {
+      if (e->scratch) IMG_HIP(hipFree(e->scratch));
+      e->scratch = nullptr;
+      e->scratch_cap = 0;
+      IMG_HIP(hipMalloc(&e->scratch, need));
+      IMG_HIP(hipMemsetAsync(e->scratch, 0, need, stream));  // the NaN word starts at epoch 0
+      e->scratch_cap = need;
+      e->epoch = 0;
+    }
+    if (((uintptr_t)rgb_dev & 15u) != 0)
+      return img_fail(SPT_ERR_INVALID_ARG, "framebuffer must be 16-byte aligned");
+    const uint32_t epoch = ++e->epoch == 0 ? ++e->epoch : e->epoch;  // never 0 (the initial word)
+    uint64_t* offs = (uint64_t*)(e->scratch + off_b);
+    uint32_t* blen = (uint32_t*)(e->scratch + len_b);
+    uint32_t* nan_word = (uint32_t*)(e->scratch + nan_b);
+    uint8_t* digits = e->scratch + dig_b;
+    const uint32_t grid1 = std::max(1u, std::min((nv / 4 + kThreads - 1) / kThreads, 2048u));
+    hipLaunchKernelGGL(p6_write, dim3(grid1), dim3(kThreads), 0, stream, (const float4*)rgb_dev, nv, T,
+                       (uint32_t*)digits, nan_word, epoch);
+    IMG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(p3_lengths, dim3(nbt), dim3(kTxtThreads), 0, stream, (const uint4*)digits, rgb_dev,
+                       nv, T, (const uint32_t*)nan_word, epoch, blen);
+    IMG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(p3_offsets, dim3(1), dim3(kScanThreads), 0, stream, (const uint32_t*)blen, nbt,
+                       (uint64_t)hd.size(), offs, e->total);
+    IMG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(p3_text, dim3(nbt), dim3(kTxtThreads), 0, stream, (const uint4*)digits, rgb_dev,
+                       nv, T, (const uint32_t*)nan_word, epoch, (const uint64_t*)offs, out_dev, cap);
     IMG_HIP(hipGetLastError());
     IMG_HIP(hipMemcpyAsync(e->h_total, e->total, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
     IMG_HIP(hipStreamSynchronize(stream));  // the text length is data-dependent
@@ -474,7 +533,7 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
       return img_fail(SPT_ERR_INVALID_ARG, "framebuffer and output must be 16-byte aligned");
     if (format == SPT_IMAGE_P6) {
       hipLaunchKernelGGL(p6_write, dim3(grid), dim3(kThreads), 0, stream, (const float4*)rgb_dev, nv, T,
-                         (uint32_t*)(out_dev + hd.size()));
+                         (uint32_t*)(out_dev + hd.size()), (uint32_t*)nullptr, 0u);
     } else if (w % 4 == 0) {
       uint32_t m, sh;
       magic31((uint32_t)w * 3 / 4, &m, &sh);
