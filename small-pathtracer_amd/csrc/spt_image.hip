@@ -147,7 +147,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
 // HBM traffic per value: 4 B read + 1 B written, 1 B read, 1 B read + 2-4 B written, with no
 // cross-block dependency inside a pass. (An image with a NaN, "-2147483648 ", takes an exact slow
 // path in the last two passes: toInt again from the floats, byte stores.)
-constexpr int kTxtThreads = 512, kTxtVals = 16, kTxtBlockVals = kTxtThreads * kTxtVals;  // 8192
+#ifndef SPT_TXT_THREADS
+#define SPT_TXT_THREADS 512
+#endif
+constexpr int kTxtThreads = SPT_TXT_THREADS, kTxtVals = 16, kTxtBlockVals = kTxtThreads * kTxtVals;  // 8192
 constexpr int kStageTxt = kTxtBlockVals * 4 + 32;  // every value <= "255 ", + the 16-byte phase
 
 // Pass 1 is the P6 kernel itself (p6_write with a NaN word: the toInt bytes, 1 B per value, and the
