@@ -8,7 +8,7 @@ ROUNDS=${ROUNDS:-2}
 for r in $(seq 1 $ROUNDS); do
   for spec in "$@"; do
     lib=${spec%%@*}; envs=""; [ "$spec" != "$lib" ] && envs=${spec#*@}
-    out=$(env SPT_LIB=$lib $envs timeout -k 10 120 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} 2>/dev/null) || { echo "$spec FAILED"; exit 1; }
+    out=$(env SPT_LIB=$lib $envs timeout -k 10 120 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} 2>gpurun_out/ab_last.err) || { echo "$spec FAILED"; exit 1; }
     echo "$spec $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["kernel_ms"])')"
   done
 done | tee gpurun_out/ab.txt
