@@ -93,3 +93,28 @@ def test_encode_into_too_small_buffer_fails(spt):
             enc.encode(rgb.data_ptr(), 4, 4, "p3", out.data_ptr(), 8)
     finally:
         enc.close()
+
+
+def test_encoder_reuse_across_nan_and_clean_images(spt, oracle):
+    """P3 in passes: a NaN anywhere sends the whole encode down the exact slow path (the encode's
+    epoch in the NaN word); the next encode with the same Encoder, without a NaN, takes the fast
+    path again. Every output byte-identical to the oracle's writer."""
+    import torch
+    h, w = 200, 311  # 186,600 values: 23 text blocks, the last one partial
+    rng = np.random.default_rng(7)
+    clean = rng.random((h, w, 3), dtype=np.float32) * 1.2 - 0.1
+    mid_nan = clean.copy()
+    mid_nan[97, 150, 1] = np.nan
+    last_nan = clean.copy()
+    last_nan[-1, -1, -1] = np.nan
+    enc = spt.Encoder(0)
+    try:
+        for img in (clean, mid_nan, clean, last_nan, clean):
+            src = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+            cap = spt.Encoder.bound(w, h, "p3")
+            out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+            n = enc.encode(src.data_ptr(), w, h, "p3", out.data_ptr(), cap)
+            torch.cuda.synchronize()
+            assert bytes(out[:n].cpu().numpy()) == oracle.encode_image(img, 0)
+    finally:
+        enc.close()
