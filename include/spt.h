@@ -235,7 +235,9 @@ uint64_t spt_image_bound(int32_t w, int32_t h, int32_t format); /* max encoded b
 spt_status spt_encoder_create(int32_t device, spt_encoder** out);
 spt_status spt_encoder_destroy(spt_encoder* enc);
 /* Encode on `stream` into out_dev (cap bytes). *len_out = encoded length. P3's length depends on
- * the data, so P3 synchronises `stream` once (after the length pass); P6/PFM do not. */
+ * the data, so P3 synchronises `stream` once (after its passes); P6/PFM do not. rgb_dev must be
+ * 16-byte aligned (SPT_ERR_INVALID_ARG otherwise; P6/PFM also need out_dev past the header 16-byte
+ * aligned). One encoder runs one encode at a time (its scratch is reused). */
 spt_status spt_encode_image(spt_encoder* enc, const float* rgb_dev, int32_t w, int32_t h,
                             int32_t format, uint8_t* out_dev, uint64_t cap, uint64_t* len_out,
                             void* stream);
