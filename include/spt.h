@@ -25,8 +25,9 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 3 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed;
-                             3: shadow_proven */
+#define SPT_ABI_VERSION 4 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed;
+                             3: shadow_proven; 4: spt_gather_plan, spt_deinterleave_source,
+                             spt_gather_staging_floats, spt_shutdown */
 
 typedef enum spt_status {
   SPT_OK = 0,
@@ -174,9 +175,16 @@ int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_t cap);
 
 /* ---- rendering ---- */
 /* One-shot drop-in for :528-542. rgb_out: caller-owned HOST buffer of shard_rows*w*3 floats
- * (linear, clamped to [0,1] per channel after the spp average, :538). stats may be NULL. */
+ * (linear, clamped to [0,1] per channel after the spp average, :538). stats may be NULL.
+ * The library keeps one render context and device output buffer per device (params.device) between
+ * calls, so repeated calls pay no context creation, allocation or cold launch; calls on one device
+ * are serialised, calls on different devices may run concurrently. Thread-safe. */
 spt_status spt_render(const spt_prim* prims, int32_t n_prims, const spt_camera* cam,
                       const spt_params* p, float* rgb_out, spt_stats* stats);
+/* Releases spt_render's cached per-device contexts and buffers (the next spt_render re-creates
+ * them). Call before unloading the library if its device memory must be returned earlier than
+ * process exit. */
+spt_status spt_shutdown(void);
 
 typedef struct spt_context spt_context;
 spt_status spt_context_create(int32_t device, spt_context** out);
@@ -216,6 +224,26 @@ spt_status spt_gather_framebuffer(spt_comm* comm, const spt_params* p, const flo
  * pointers on the current device), image_dev = h*w*3 floats. */
 spt_status spt_deinterleave_rows(const spt_params* p, int32_t nranks, const float* const* shards_dev,
                                  float* image_dev, void* stream);
+/* The gather as pure host functions (no device, no RCCL; spt_gather_framebuffer executes exactly
+ * this plan): the transfers `rank` posts inside the gather's ncclGroupStart/End. Rank k > 0 sends
+ * its compact shard (count = its rows * w * 3 floats) to rank 0; rank 0 receives each rank k > 0
+ * that owns rows into its staging buffer at offset (k - 1) * (shard 0's floats) -- shard 0 never
+ * owns fewer rows than another shard. Returns the number of ops (<= cap), or -1 on bad arguments
+ * or a too small cap. */
+typedef struct spt_gather_op {
+  int32_t kind;    /* SPT_GATHER_SEND or SPT_GATHER_RECV */
+  int32_t peer;    /* the other rank */
+  uint64_t count;  /* floats */
+  uint64_t offset; /* RECV: float offset into rank 0's staging buffer; SEND: 0 */
+} spt_gather_op;
+enum { SPT_GATHER_SEND = 0, SPT_GATHER_RECV = 1 };
+int32_t spt_gather_plan(const spt_params* p, int32_t nranks, int32_t rank, spt_gather_op* ops,
+                        int32_t cap);
+uint64_t spt_gather_staging_floats(const spt_params* p, int32_t nranks); /* rank 0's staging size */
+/* Where rank 0's de-interleave reads image row `row`: shard *rank's compact row *compact_row (the
+ * device kernel's own row map). */
+spt_status spt_deinterleave_source(const spt_params* p, int32_t nranks, int32_t row, int32_t* rank,
+                                   int32_t* compact_row);
 /* One process driving n_dev GPUs (smallpt_amd --devices N): shard k renders on devices[k]
  * (distinct), the gather lands on devices[0], rgb_out = the full image on the host (h*w*3 floats).
  * p's shard fields are ignored. stats: summed over devices, kernel_ms = the slowest device's. */

@@ -44,6 +44,8 @@ def lib() -> ctypes.CDLL:
         L.spt_oracle_erand48.restype = ctypes.c_double
         L.spt_oracle_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, P(ctypes.c_int32)]
         L.spt_oracle_philox.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
+        L.spt_oracle_philox_r.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32),
+                                          ctypes.c_int]
         L.spt_oracle_set_pairs.argtypes = [ctypes.c_int]
         L.spt_oracle_disk_dir.argtypes = [ctypes.c_uint32, P(ctypes.c_float), P(ctypes.c_float)]
         L.spt_oracle_sincos2pi.argtypes = [ctypes.c_float, P(ctypes.c_float), P(ctypes.c_float)]
@@ -214,6 +216,15 @@ def philox(ctr, key):
     k = (ctypes.c_uint32 * 2)(*key)
     o = (ctypes.c_uint32 * 4)()
     lib().spt_oracle_philox(c, k, o)
+    return list(o)
+
+
+def philox_r(ctr, key, rounds: int):
+    """Philox4x32 with `rounds` rounds (the contract uses SPT_PHILOX_ROUNDS = 7)."""
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().spt_oracle_philox_r(c, k, o, rounds)
     return list(o)
 
 

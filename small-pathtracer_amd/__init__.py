@@ -86,6 +86,13 @@ class spt_stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class spt_gather_op(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("count", ctypes.c_uint64),
+                ("offset", ctypes.c_uint64)]
+
+
+GATHER_SEND, GATHER_RECV = 0, 1
+
 STAT_KEYS = ["samples", "path_rays", "shadow_rays", "vertices", "nee_events", "nee_light_hits",
              "cosine_samples", "misses", "shadow_traced", "sphere_vertices"]
 
@@ -97,7 +104,8 @@ EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_sc
            "spt_status_string", "spt_last_error", "spt_device_count", "spt_image_bound",
            "spt_encoder_create", "spt_encoder_destroy", "spt_encode_image", "spt_write_image",
            "spt_comm_unique_id", "spt_comm_create", "spt_comm_destroy", "spt_comm_reserve",
-           "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi"]
+           "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi", "spt_shutdown",
+           "spt_gather_plan", "spt_gather_staging_floats", "spt_deinterleave_source"]
 IMAGE_FORMATS = {"p3": 0, "p6": 1, "pfm": 2}
 FLAG_UNIFORM_SCATTER = 1  # spt_params.flags: random_scattering from the uniform code of :352-359
 # spt_params.flags bits 8-9: cap on the kernel specialisation (A/B and tests; never changes results).
@@ -172,8 +180,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.spt_deinterleave_rows.argtypes = [P(spt_params), I32, P(VP), VP, VP]
     lib.spt_render_multi.argtypes = [P(spt_prim), I32, P(spt_camera), P(spt_params), P(I32), I32,
                                      P(ctypes.c_float), P(spt_stats)]
+    lib.spt_gather_plan.argtypes = [P(spt_params), I32, I32, P(spt_gather_op), I32]
+    lib.spt_gather_plan.restype = I32
+    lib.spt_gather_staging_floats.argtypes = [P(spt_params), I32]
+    lib.spt_gather_staging_floats.restype = U64
+    lib.spt_deinterleave_source.argtypes = [P(spt_params), I32, I32, P(I32), P(I32)]
+    lib.spt_shutdown.argtypes = []
     for name in ("spt_comm_unique_id", "spt_comm_create", "spt_comm_destroy", "spt_comm_reserve",
-                 "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi"):
+                 "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi",
+                 "spt_deinterleave_source", "spt_shutdown"):
         getattr(lib, name).restype = I32
     for name in ("spt_default_params", "spt_camera_init", "spt_scene_cornell",
                  "spt_scene_spheres32", "spt_scene_cornell_specular", "spt_scene_smallpt_classic",
@@ -457,6 +472,33 @@ class Comm:
                                                ctypes.c_void_p(shard_dev_ptr),
                                                ctypes.c_void_p(image_dev_ptr or None),
                                                ctypes.c_void_p(stream_ptr or None)))
+
+
+def gather_plan(params: spt_params, nranks: int, rank: int) -> list:
+    """spt_gather_plan(): the (kind, peer, count, offset) transfers `rank` posts in one framebuffer
+    gather (pure host function, no device)."""
+    ops = (spt_gather_op * 64)()
+    n = load_library().spt_gather_plan(ctypes.byref(params), int(nranks), int(rank), ops, 64)
+    if n < 0:
+        raise SptError(1, "spt_gather_plan: bad arguments")
+    return [(ops[i].kind, ops[i].peer, int(ops[i].count), int(ops[i].offset)) for i in range(n)]
+
+
+def gather_staging_floats(params: spt_params, nranks: int) -> int:
+    return int(load_library().spt_gather_staging_floats(ctypes.byref(params), int(nranks)))
+
+
+def deinterleave_source(params: spt_params, nranks: int, row: int) -> tuple:
+    """(rank, compact row) the de-interleave kernel reads image row `row` from."""
+    k, j = ctypes.c_int32(), ctypes.c_int32()
+    _check(load_library().spt_deinterleave_source(ctypes.byref(params), int(nranks), int(row),
+                                                  ctypes.byref(k), ctypes.byref(j)))
+    return k.value, j.value
+
+
+def shutdown() -> None:
+    """spt_shutdown(): release spt_render's cached per-device contexts."""
+    _check(load_library().spt_shutdown())
 
 
 def deinterleave_rows(params: spt_params, shard_dev_ptrs, image_dev_ptr: int, stream_ptr: int = 0):

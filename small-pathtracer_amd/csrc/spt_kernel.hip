@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <utility>
 
@@ -34,6 +35,9 @@
 #include "spt_device.h"
 #include "spt_cornell.h"
 #include "spt_diag.h"
+
+#define SPT_STR_(x) #x
+#define SPT_XSTR(x) SPT_STR_(x)
 
 namespace spt {
 
@@ -938,6 +942,12 @@ render_kernel(const KParams* __restrict__ Pg) {
     if (ls >= kStPath) {  // kStPath or kStShadow
       // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
       SPT_REGION(4);
+#ifdef SPT_PROBE_SALU  // A/B probe: N extra SALU per wave-iteration (marginal issue cost)
+      { uint32_t z_ = iter; asm volatile(".rept " SPT_XSTR(SPT_PROBE_SALU) "\n s_add_u32 %0, %0, 1\n .endr" : "+s"(z_)); }
+#endif
+#ifdef SPT_PROBE_VALU  // A/B probe: N extra VALU per wave-iteration
+      { float z_ = o.x; asm volatile(".rept " SPT_XSTR(SPT_PROBE_VALU) "\n v_add_f32 %0, 1.0, %0\n .endr" : "+v"(z_)); }
+#endif
       const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
       int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
       float t, ia_hit;
@@ -1967,38 +1977,75 @@ extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   return SPT_OK;
 }
 
+// The one-shot drop-in (spt_render) keeps one context and one device output buffer per device for
+// the life of the process (or until spt_shutdown), so a caller that renders repeatedly -- the
+// reference's main() replaced by smallpt_amd, or a Python loop over spt.render -- pays context
+// creation, the unit-slot allocation (~200 MB at C3) and the cold first launch once, not per call.
+// Calls on one device are serialised by that device's mutex; different devices run concurrently.
+namespace {
+constexpr int kMaxDropInDevices = 64;
+struct DropIn {
+  std::mutex mu;
+  spt_context* ctx = nullptr;
+  float* out = nullptr;  // device output, grown on demand
+  size_t out_cap = 0;    // floats
+};
+DropIn g_dropin[kMaxDropInDevices];
+}  // namespace
+
 extern "C" spt_status spt_render(const spt_prim* prims, int32_t n_prims, const spt_camera* cam,
                                  const spt_params* p, float* rgb_out, spt_stats* stats) {
   if (!rgb_out) return fail(SPT_ERR_INVALID_ARG, "null rgb_out");
   spt_status st = validate(prims, n_prims, cam, p);
   if (st != SPT_OK) return st;
-  spt_context* c = nullptr;
-  st = spt_context_create(p->device, &c);
-  if (st != SPT_OK) return st;
+  if (p->device < 0 || p->device >= kMaxDropInDevices) return fail(SPT_ERR_INVALID_ARG, "bad device ordinal");
+  DropIn& D = g_dropin[p->device];
+  std::lock_guard<std::mutex> lock(D.mu);
+  if (!D.ctx) {
+    st = spt_context_create(p->device, &D.ctx);
+    if (st != SPT_OK) {
+      D.ctx = nullptr;
+      return st;
+    }
+  }
   const size_t n = 3ull * (size_t)spt_shard_row_count(p) * (size_t)p->width;
   if (n == 0) {  // this shard owns no rows
     if (stats) std::memset(stats, 0, sizeof *stats);
-    spt_context_destroy(c);
     return SPT_OK;
   }
-  float* dev = nullptr;
-  hipError_t e = hipMalloc(&dev, n * sizeof(float));
-  if (e != hipSuccess) {
-    spt_context_destroy(c);
-    return fail(SPT_ERR_OOM, "output alloc");
+  SPT_HIP(hipSetDevice(p->device));
+  if (n > D.out_cap) {
+    if (D.out) SPT_HIP(hipFree(D.out));
+    D.out = nullptr;
+    D.out_cap = 0;
+    SPT_HIP(hipMalloc(&D.out, n * sizeof(float)));
+    D.out_cap = n;
   }
-  st = spt_render_async(c, prims, n_prims, cam, p, dev, nullptr);
+  st = spt_render_async(D.ctx, prims, n_prims, cam, p, D.out, nullptr);
   if (st == SPT_OK) {
     spt_stats tmp;
-    st = spt_context_stats(c, stats ? stats : &tmp);
+    st = spt_context_stats(D.ctx, stats ? stats : &tmp);
   }
-  if (st == SPT_OK) {
-    e = hipMemcpy(rgb_out, dev, n * sizeof(float), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) st = fail(SPT_ERR_HIP, hipGetErrorString(e));
-  }
-  (void)hipFree(dev);
-  spt_context_destroy(c);
+  if (st == SPT_OK) SPT_HIP(hipMemcpy(rgb_out, D.out, n * sizeof(float), hipMemcpyDeviceToHost));
   return st;
+}
+
+extern "C" spt_status spt_shutdown(void) {
+  for (DropIn& D : g_dropin) {
+    std::lock_guard<std::mutex> lock(D.mu);
+    if (D.ctx) {
+      const int dev = D.ctx->device;
+      spt_context_destroy(D.ctx);
+      D.ctx = nullptr;
+      if (D.out) {
+        (void)hipSetDevice(dev);
+        (void)hipFree(D.out);
+      }
+    }
+    D.out = nullptr;
+    D.out_cap = 0;
+  }
+  return SPT_OK;
 }
 
 extern "C" int32_t spt_device_count(void) {

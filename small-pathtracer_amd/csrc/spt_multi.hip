@@ -52,14 +52,24 @@ spt_status fail(spt_status s, const std::string& msg) {
 
 struct Sources { const float* p[kMaxRanks]; };
 
-// image row r (tile t = r / T, rank t % n, that rank's tile t / n) <- the rank's compact row
-// (t / n) * T + r % T. One block per image row, 16-byte vectors when a row is a multiple of them.
+// The de-interleave's row map, shared by the kernel and the host plan (spt_deinterleave_source):
+// image row r lies in tile t = r / T, which rank k = t % n rendered as its compact row
+// j = (t / n) * T + r % T (spt_shard_rows lists a shard's rows in increasing order).
+__host__ __device__ inline void row_source(int r, int n, int T, int* k, size_t* j) {
+  const int t = r / T;
+  *k = t % n;
+  *j = (size_t)(t / n) * (size_t)T + (size_t)(r % T);
+}
+
+// image row r <- its rank's compact row (row_source). One block per image row, 16-byte vectors when
+// a row is a multiple of them.
 __global__ void __launch_bounds__(kThreads)
 deinterleave_kernel(Sources src, int n, int T, int h, int row_floats, float* __restrict__ image) {
   const int r = blockIdx.x;
   if (r >= h) return;
-  const int t = r / T, k = t % n;
-  const size_t j = (size_t)(t / n) * T + (size_t)(r % T);
+  int k;
+  size_t j;
+  row_source(r, n, T, &k, &j);
   const float* __restrict__ s = src.p[k] + j * (size_t)row_floats;
   float* __restrict__ d = image + (size_t)r * (size_t)row_floats;
   if ((row_floats & 3) == 0 && ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
@@ -115,6 +125,49 @@ extern "C" spt_status spt_deinterleave_rows(const spt_params* p, int32_t nranks,
   return SPT_OK;
 }
 
+// ---- the gather as pure host functions (CPU-testable: no device, no RCCL) ----
+
+extern "C" uint64_t spt_gather_staging_floats(const spt_params* p, int32_t nranks) {
+  if (check_layout(p, nranks) != SPT_OK) return 0;
+  return nranks < 2 ? 0 : shard_floats(p, 0) * (uint64_t)(nranks - 1);
+}
+
+extern "C" int32_t spt_gather_plan(const spt_params* p, int32_t nranks, int32_t rank,
+                                   spt_gather_op* ops, int32_t cap) {
+  if (check_layout(p, nranks) != SPT_OK || rank < 0 || rank >= nranks || cap < 0 || (!ops && cap > 0))
+    return -1;
+  // slot = shard 0's floats: shard 0 owns tiles 0, n, 2n, ..., never fewer rows than another shard
+  const uint64_t slot = shard_floats(p, 0);
+  int32_t n = 0;
+  auto put = [&](int32_t kind, int32_t peer, uint64_t count, uint64_t offset) {
+    if (n < cap) ops[n] = spt_gather_op{kind, peer, count, offset};
+    ++n;
+  };
+  if (rank != 0) {
+    const uint64_t cnt = shard_floats(p, rank);
+    if (cnt) put(SPT_GATHER_SEND, 0, cnt, 0);
+  } else {
+    for (int k = 1; k < nranks; ++k) {
+      const uint64_t cnt = shard_floats(p, k);
+      if (cnt) put(SPT_GATHER_RECV, k, cnt, (uint64_t)(k - 1) * slot);
+    }
+  }
+  return n > cap ? -1 : n;
+}
+
+extern "C" spt_status spt_deinterleave_source(const spt_params* p, int32_t nranks, int32_t row,
+                                              int32_t* rank, int32_t* compact_row) {
+  spt_status st = check_layout(p, nranks);
+  if (st != SPT_OK) return st;
+  if (!rank || !compact_row || row < 0 || row >= p->height) return fail(SPT_ERR_INVALID_ARG, "bad row");
+  int k;
+  size_t j;
+  row_source(row, nranks, tile_rows_of(p), &k, &j);
+  *rank = k;
+  *compact_row = (int32_t)j;
+  return SPT_OK;
+}
+
 extern "C" spt_status spt_comm_unique_id(uint8_t id[SPT_COMM_ID_BYTES]) {
   if (!id) return fail(SPT_ERR_INVALID_ARG, "null id");
   static_assert(SPT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
@@ -154,18 +207,17 @@ extern "C" spt_status spt_comm_destroy(spt_comm* c) {
 
 namespace {
 
-// The transfers of one gather as calls inside an open ncclGroupStart/End: rank k > 0 sends its
-// compact shard to rank 0; rank 0 posts one receive per other rank into its slot of gbuf.
-spt_status post_gather(spt_comm* c, const spt_params* p, const float* shard_dev, hipStream_t s,
-                       size_t slot) {
-  if (c->rank != 0) {
-    const size_t n = shard_floats(p, c->rank);
-    if (n) SPT_NCCL(ncclSend(shard_dev, n, ncclFloat32, 0, c->comm, s));
-    return SPT_OK;
-  }
-  for (int k = 1; k < c->nranks; ++k) {
-    const size_t n = shard_floats(p, k);
-    if (n) SPT_NCCL(ncclRecv(c->gbuf + (size_t)(k - 1) * slot, n, ncclFloat32, k, c->comm, s));
+// The transfers of one gather as calls inside an open ncclGroupStart/End, executed from the pure
+// host plan (spt_gather_plan): rank k > 0 sends its compact shard to rank 0; rank 0 posts one
+// receive per other rank into that rank's slot of gbuf.
+spt_status post_gather(spt_comm* c, const spt_params* p, const float* shard_dev, hipStream_t s) {
+  spt_gather_op ops[kMaxRanks];
+  const int n_ops = spt_gather_plan(p, c->nranks, c->rank, ops, kMaxRanks);
+  if (n_ops < 0) return fail(SPT_ERR_INVALID_ARG, "gather plan");
+  for (int i = 0; i < n_ops; ++i) {
+    const spt_gather_op& o = ops[i];
+    if (o.kind == SPT_GATHER_SEND) SPT_NCCL(ncclSend(shard_dev, o.count, ncclFloat32, o.peer, c->comm, s));
+    else SPT_NCCL(ncclRecv(c->gbuf + o.offset, o.count, ncclFloat32, o.peer, c->comm, s));
   }
   return SPT_OK;
 }
@@ -183,11 +235,16 @@ spt_status reserve_gbuf(spt_comm* c, size_t slot) {
   return SPT_OK;
 }
 
+// Rank 0's de-interleave: shard 0 from its own render, shard k > 0 from where the plan's receive
+// from k landed (a rank that owns no rows has no receive, and the de-interleave reads none of it).
 spt_status deinterleave_on_root(spt_comm* c, const spt_params* p, const float* shard_dev,
-                                float* image_dev, hipStream_t s, size_t slot) {
-  std::vector<const float*> src((size_t)c->nranks);
+                                float* image_dev, hipStream_t s) {
+  std::vector<const float*> src((size_t)c->nranks, (const float*)c->gbuf);
   src[0] = shard_dev;
-  for (int k = 1; k < c->nranks; ++k) src[(size_t)k] = c->gbuf + (size_t)(k - 1) * slot;
+  spt_gather_op ops[kMaxRanks];
+  const int n_ops = spt_gather_plan(p, c->nranks, 0, ops, kMaxRanks);
+  if (n_ops < 0) return fail(SPT_ERR_INVALID_ARG, "gather plan");
+  for (int i = 0; i < n_ops; ++i) src[(size_t)ops[i].peer] = c->gbuf + ops[i].offset;
   return spt_deinterleave_rows(p, c->nranks, src.data(), image_dev, s);
 }
 
@@ -215,12 +272,12 @@ extern "C" spt_status spt_gather_framebuffer(spt_comm* c, const spt_params* p,
   const hipStream_t s = (hipStream_t)stream;
   if (c->nranks > 1) {
     SPT_NCCL(ncclGroupStart());
-    st = post_gather(c, p, shard_dev, s, slot);
+    st = post_gather(c, p, shard_dev, s);
     const ncclResult_t r = ncclGroupEnd();
     if (st != SPT_OK) return st;
     if (r != ncclSuccess) return fail(SPT_ERR_RCCL, std::string("ncclGroupEnd: ") + ncclGetErrorString(r));
   }
-  if (c->rank == 0) return deinterleave_on_root(c, p, shard_dev, image_dev, s, slot);
+  if (c->rank == 0) return deinterleave_on_root(c, p, shard_dev, image_dev, s);
   return SPT_OK;
 }
 
@@ -300,14 +357,14 @@ extern "C" spt_status spt_render_multi(const spt_prim* prims, int32_t n_prims, c
     for (int k = 0; k < n_dev && st == SPT_OK; ++k) {
       Rank& r = R[(size_t)k];
       spt_params q = base;
-      st = post_gather(&r.comm, &q, r.shard, r.stream, slot);
+      st = post_gather(&r.comm, &q, r.shard, r.stream);
     }
     const ncclResult_t e = ncclGroupEnd();
     if (st == SPT_OK && e != ncclSuccess) st = fail(SPT_ERR_RCCL, std::string("ncclGroupEnd: ") + ncclGetErrorString(e));
   }
   if (st == SPT_OK) {
     (void)hipSetDevice(devices[0]);
-    st = deinterleave_on_root(&R[0].comm, &base, R[0].shard, image, R[0].stream, slot);
+    st = deinterleave_on_root(&R[0].comm, &base, R[0].shard, image, R[0].stream);
   }
   spt_stats tot{};
   for (int k = 0; k < n_dev && st == SPT_OK; ++k) {

@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol(spt):
 
 def test_abi_version_and_status_strings(spt):
     lib = spt.load_library()
-    assert lib.spt_abi_version() == 3
+    assert lib.spt_abi_version() == 4
     for code, text in spt.STATUS.items():
         assert lib.spt_status_string(code).decode() == text
 

@@ -418,3 +418,19 @@ def test_random_scenes_bit_exact(spt, oracle, seed, n_rect, n_sph, mats, nee):
     _assert_exact(gpu, cpu)
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
     assert gst["samples"] == 40 * 30 * 6
+
+
+def test_dropin_render_reuses_its_context(spt, oracle):
+    """spt_render keeps one context per device between calls (include/spt.h): repeated calls of
+    different sizes, a spt_shutdown in between and a re-created context all give the oracle's
+    image and statistics bit for bit."""
+    prims = spt.cornell_scene()
+    for (w, h, spp, seed) in [(40, 30, 8, 3), (64, 48, 16, 1), (40, 30, 8, 3), (17, 9, 5, 2)]:
+        p = spt.default_params(width=w, height=h, spp=spp, seed=seed)
+        gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+        _assert_exact(gpu, cpu)
+        assert all(gst[k] == cst[k] for k in spt.STAT_KEYS)
+        if (w, h) == (64, 48):
+            spt.shutdown()
+    spt.shutdown()
+    spt.shutdown()  # idempotent

@@ -85,3 +85,46 @@ def test_shard_zero_is_the_largest_shard(spt):
                 assert sd.max_rows(sd.shard_row_lists(h, t, n)) == counts[0]
                 cases += 1
     assert cases > 3000
+
+
+def test_gather_plan_reassembles_image(spt):
+    """The transfers spt_gather_framebuffer posts (spt_gather_plan: what spt_multi.hip executes
+    inside its ncclGroupStart/End) and the de-interleave's row map (spt_deinterleave_source: the
+    kernel's own row_source), simulated on the host for every (h, tile, n <= 8): every send has a
+    matching receive of the same size, the receives land in disjoint slots inside rank 0's staging
+    buffer, and de-interleaving from shard 0 and the staging buffer rebuilds every image row."""
+    w = 3
+    cases = 0
+    for h in list(range(1, 41)) + [95, 96, 97, 767, 768, 769]:
+        for t in (1, 2, 3, 7, 8, 16):
+            for n in range(1, 9):
+                ps = [spt.default_params(width=w, height=h, spp=1, tile_rows=t, shard_index=k,
+                                         shard_count=n) for k in range(n)]
+                rows = [spt.shard_rows(p) for p in ps]
+                # shard k's compact buffer: row r's 3*w floats all hold r
+                shards = [np.repeat(r.astype(np.float64), 3 * w) for r in rows]
+                staging = np.full(spt.gather_staging_floats(ps[0], n), -1.0)
+                sends = {}
+                for k in range(1, n):
+                    plan = spt.gather_plan(ps[k], n, k)
+                    assert all(op[0] == spt.GATHER_SEND and op[1] == 0 and op[3] == 0 for op in plan)
+                    assert [op[2] for op in plan] == ([len(rows[k]) * 3 * w] if len(rows[k]) else [])
+                    if plan:
+                        sends[k] = plan[0][2]
+                recvs = spt.gather_plan(ps[0], n, 0)
+                assert {op[1]: op[2] for op in recvs} == sends
+                src = {0: (shards[0], 0)}
+                used = np.zeros(len(staging), dtype=bool)
+                for kind, peer, count, off in recvs:
+                    assert kind == spt.GATHER_RECV and off + count <= len(staging)
+                    assert not used[off:off + count].any()
+                    used[off:off + count] = True
+                    staging[off:off + count] = shards[peer]  # the transfer
+                    src[peer] = (staging, off)
+                for r in range(h):
+                    k, j = spt.deinterleave_source(ps[0], n, r)
+                    buf, off = src[k]
+                    seg = buf[off + j * 3 * w: off + (j + 1) * 3 * w]
+                    assert len(seg) == 3 * w and (seg == r).all(), (h, t, n, r, k, j)
+                cases += 1
+    assert cases > 2000

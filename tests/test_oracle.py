@@ -111,6 +111,36 @@ def test_philox_random123_kat(oracle):
         assert oracle.philox(kat["ctr"], kat["key"]) == kat["out"]
 
 
+def _philox_py(ctr, key, rounds):
+    """Philox4x32-R as published (Salmon et al., SC'11, Random123's constants), in Python big-integer
+    arithmetic: an implementation independent of the oracle's C (spt_oracle_philox_r)."""
+    m0, m1, w0, w1, mask = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85, 0xFFFFFFFF
+    x, (k0, k1) = list(ctr), key
+    for _ in range(rounds):
+        p0, p1 = m0 * x[0], m1 * x[2]
+        x = [((p1 >> 32) ^ x[1] ^ k0) & mask, p1 & mask, ((p0 >> 32) ^ x[3] ^ k1) & mask, p0 & mask]
+        k0, k1 = (k0 + w0) & mask, (k1 + w1) & mask
+    return x
+
+
+def test_philox7_known_answers(oracle):
+    """The contract's generator at its own round count (SPT_PHILOX_ROUNDS = 7, include/spt.h): the
+    Python restatement reproduces Random123's 10-round vectors, and the committed 7-round vectors it
+    made (golden.json philox4x32_7) equal both it and the oracle's C function."""
+    hdr = open(os.path.join(os.path.dirname(HERE), "include", "spt.h")).read()
+    assert "#define SPT_PHILOX_ROUNDS 7" in hdr
+    for kat in GOLD["kat"]["philox4x32_10"]:
+        assert _philox_py(kat["ctr"], kat["key"], 10) == kat["out"]
+    for kat in GOLD["kat"]["philox4x32_7"]:
+        assert _philox_py(kat["ctr"], kat["key"], 7) == kat["out"]
+        assert oracle.philox_r(kat["ctr"], kat["key"], 7) == kat["out"]
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        ctr = [int(v) for v in rng.integers(0, 1 << 32, 4)]
+        key = [int(v) for v in rng.integers(0, 1 << 32, 2)]
+        assert oracle.philox_r(ctr, key, 7) == _philox_py(ctr, key, 7)
+
+
 @pytest.mark.parametrize("aspect,key", [(1.0, "camera_aspect1"), (4 / 3, "camera_aspect4_3")])
 def test_camera_kat(oracle, aspect, key):
     c = oracle.camera(aspect)
