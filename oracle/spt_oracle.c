@@ -460,15 +460,17 @@ static void c_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_
 
 typedef struct { float x, y, z; } fv;
 static inline fv fv3(float x, float y, float z) { fv r = {x, y, z}; return r; }
-static inline float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
-static inline float u16(uint32_t lo, uint32_t hi) {
-  return (float)((lo & 0xFFu) | ((hi & 0xFFu) << 8)) * 0x1p-16f;
-}
+static inline uint32_t u16i(uint32_t lo, uint32_t hi) { return (lo & 0xFFu) | ((hi & 0xFFu) << 8); }
+static inline float u16(uint32_t lo, uint32_t hi) { return (float)u16i(lo, hi) * 0x1p-16f; }
 static inline float fdot(fv a, fv b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 /* Deterministic reciprocal / rsqrt of the contract: integer seed + 3 Newton steps (only IEEE
  * fma/mul and integer ops, so every platform computes the same bits). */
 static inline float asf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static inline uint32_t asu(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+/* Contract v5: a uniform [0, 1) float from the top 23 bits of a Philox word, built as the float
+ * 1 + m * 2^-23 (bits 0x3F800000 | m) minus 1 -- exact; on the GPU an or and a subtract instead of a
+ * shift, a half-rate conversion and a multiply (rounds 1-4: (v >> 8) * 2^-24). */
+static inline float u01(uint32_t v) { return asf(0x3F800000u | (v >> 9)) - 1.0f; }
 float spt_oracle_rcp_nr(float x) {
   float y = asf(0x7EF311C3u - asu(x));
   int i;
@@ -609,6 +611,7 @@ typedef struct {
   int kind;
   float k0, k1, ma, ha, mb, hb;
   int id0, id1;
+  int pos0, pos1; /* grouped positions of the two planes (the nearest-hit key's low bits, c_key) */
 } c_test;
 
 typedef struct {
@@ -618,6 +621,12 @@ typedef struct {
   uint32_t key[2];
   const c_test* tests; /* rect tests in contract order (c_build_tests) */
   int n_tests;
+  int pos2idx[64];      /* grouped position -> primitive index: rects XY, XZ, YZ (index order
+                           inside a kind), then spheres (narrow, then wide, index order) */
+  int n_rect;           /* rectangles = the first sphere's position */
+  int light_pos;        /* grouped position of P->light_id (-1: none) */
+  int room[3];          /* tests of the scene's room (c_find_room), -1 = none */
+  float room_m[3], room_h[3]; /* room box per axis x, y, z: mid and half + 2^-8 */
   int unit;     /* c_unit_dirs: 1 = unit directions, 0 = the free-scale contract */
   float nee_c;  /* free-scale NEE weight constant: light_area / pi, rounded once */
 } c_ctx;
@@ -641,6 +650,7 @@ static int c_unit_dirs(const spt_prim* s, int n) {
   return 0;
 }
 static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T);
+static void c_find_room(c_ctx* C, const spt_prim* s);
 static int g_unit_override = -1; /* test hook: -1 = the contract (c_unit_dirs), 0/1 = forced */
 void spt_oracle_set_unit_dirs(int mode) { g_unit_override = mode; }
 static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n, const spt_params* P,
@@ -648,6 +658,23 @@ static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n,
   C->prims = CP; C->n = n; C->P = P; C->key[0] = SPT_PHILOX_KEY0; C->key[1] = SPT_PHILOX_KEY1;
   C->n_tests = c_build_tests(CP, n, P->light_id, CT);
   C->tests = CT;
+  {
+    int i, kind, pos = 0;
+    for (kind = SPT_RECT_XY; kind <= SPT_RECT_YZ; kind++)
+      for (i = 0; i < n; i++)
+        if (CP[i].kind == kind) C->pos2idx[pos++] = i;
+    C->n_rect = pos;
+    for (kind = 0; kind < 2; kind++) /* narrow spheres, then wide ones */
+      for (i = 0; i < n; i++)
+        if (CP[i].kind == SPT_SPHERE && CP[i].wide == kind) C->pos2idx[pos++] = i;
+  }
+  c_find_room(C, prims);
+  {
+    int i;
+    C->light_pos = -1;
+    for (i = 0; i < n; i++)
+      if (C->pos2idx[i] == P->light_id) C->light_pos = i;
+  }
   C->unit = g_unit_override >= 0 ? g_unit_override : c_unit_dirs(prims, n);
   C->nee_c = (float)((double)P->light_area / 3.14159265358979323846);
 }
@@ -661,7 +688,10 @@ static int g_pairs = 1;
  * rule must reproduce), 1 = the contract. Not thread-safe against a running render. */
 void spt_oracle_set_pairs(int on) { g_pairs = on != 0; }
 static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
-  int used[64] = {0}, nt = 0, kind, i, j;
+  int used[64] = {0}, gpos[64], nt = 0, kind, i, j, g = 0;
+  for (kind = SPT_RECT_XY; kind <= SPT_RECT_YZ; kind++)
+    for (i = 0; i < n; i++)
+      if (P[i].kind == kind) gpos[i] = g++;
   for (kind = SPT_RECT_XY; kind <= SPT_RECT_YZ; kind++) {
     for (i = 0; i < n; i++) {
       const c_prim* A = &P[i];
@@ -673,6 +703,7 @@ static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
       t->k0 = t->k1 = A->k;
       t->ma = A->ma; t->ha = A->ha; t->mb = A->mb; t->hb = A->hb;
       t->id0 = t->id1 = i;
+      t->pos0 = t->pos1 = gpos[i];
       if (i == light_id) continue;
       if (!g_pairs) continue; /* diagnostic: every rectangle tested on its own */
       for (j = i + 1; j < n; j++) {
@@ -682,14 +713,63 @@ static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
             asu(B->hb) != asu(A->hb) || asu(B->k) == asu(A->k) || !(B->k == B->k) || !(A->k == A->k))
           continue;
         used[j] = 1;
-        if (A->k < B->k) { t->k1 = B->k; t->id1 = j; }
-        else { t->k0 = B->k; t->id0 = j; t->k1 = A->k; t->id1 = i; }
+        if (A->k < B->k) { t->k1 = B->k; t->id1 = j; t->pos1 = gpos[j]; }
+        else { t->k0 = B->k; t->id0 = j; t->pos0 = gpos[j]; t->k1 = A->k; t->id1 = i; t->pos1 = gpos[i]; }
         break;
       }
     }
   }
   return nt;
 }
+
+/* Contract v5: the scene's ROOM, if it has one -- three parallel pairs, one per kind, that close a
+ * box: the XY pair's planes z = {z1, z2}, the XZ pair's y = {y1, y2} and the YZ pair's x = {x1, x2}
+ * are exactly (in the caller's doubles) the other pairs' in-plane bounds (the reference's walls
+ * :288-293: x [1, 99], y [0, 81.6], z [0, 170]). The first such triple in test order. */
+static int c_same_range(double a1, double a2, double b1, double b2) {
+  const double lo = a1 < a2 ? a1 : a2, hi = a1 < a2 ? a2 : a1;
+  return lo == b1 && hi == b2;
+}
+static void c_find_room(c_ctx* C, const spt_prim* s) {
+  int a, b, c;
+  C->room[0] = C->room[1] = C->room[2] = -1;
+  for (a = 0; a < C->n_tests; a++) {
+    const c_test* A = &C->tests[a]; /* XY: bounds x (geom 0,1), y (geom 2,3); planes z */
+    if (A->kind != SPT_RECT_XY || A->id0 == A->id1) continue;
+    for (b = 0; b < C->n_tests; b++) {
+      const c_test* B = &C->tests[b]; /* XZ: bounds x, z; planes y */
+      if (B->kind != SPT_RECT_XZ || B->id0 == B->id1) continue;
+      for (c = 0; c < C->n_tests; c++) {
+        const c_test* D = &C->tests[c]; /* YZ: bounds y, z; planes x */
+        const double* ga = s[A->id0].geom, *gb = s[B->id0].geom, *gd = s[D->id0].geom;
+        if (D->kind != SPT_RECT_YZ || D->id0 == D->id1) continue;
+        if (!c_same_range(s[D->id0].geom[4], s[D->id1].geom[4], ga[0], ga[1]) ||
+            !c_same_range(s[D->id0].geom[4], s[D->id1].geom[4], gb[0], gb[1]) ||
+            !c_same_range(s[B->id0].geom[4], s[B->id1].geom[4], ga[2], ga[3]) ||
+            !c_same_range(s[B->id0].geom[4], s[B->id1].geom[4], gd[0], gd[1]) ||
+            !c_same_range(s[A->id0].geom[4], s[A->id1].geom[4], gb[2], gb[3]) ||
+            !c_same_range(s[A->id0].geom[4], s[A->id1].geom[4], gd[2], gd[3]))
+          continue;
+        C->room[0] = a; C->room[1] = b; C->room[2] = c;
+        C->room_m[0] = A->ma; C->room_h[0] = A->ha + 0x1p-8f;
+        C->room_m[1] = A->mb; C->room_h[1] = A->hb + 0x1p-8f;
+        C->room_m[2] = B->mb; C->room_h[2] = B->hb + 0x1p-8f;
+        return;
+      }
+    }
+  }
+}
+
+/* Contract v5: the nearest-hit key of a candidate at t on the plane (or sphere) with grouped
+ * position pos: the float bits of t minus one (so 0 < t < tmin stays ONE unsigned compare, +-0,
+ * negatives, inf and NaN rank last) with the low 6 bits replaced by pos. The nearest hit is the
+ * smallest key: a candidate's t is ranked to 64 ulps, ties and near-ties inside that resolve to
+ * the lower position (the reference: strict `<` over rect[] :328, ties to the lower index). On the
+ * GPU a key is one v_add and one v_bitop3, and the running minimum one v_min_u32 -- no compare and
+ * lane-mask select per candidate. */
+static inline uint32_t c_key(float t, int pos) { return ((asu(t) - 1u) | 63u) ^ (uint32_t)(63 - pos); }
+#define C_KEY_NONE ((asu(1e20f) - 1u) | 63u) /* tmin = 1e20 (:324): no hit */
+static inline uint32_t c_umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 /* The counter-mode scene intersection (intersect :323-335). inv = rcp_nr(d) once per ray.
  * The rect tests (c_build_tests) run in their contract order — kind XY, XZ, YZ — then the spheres
@@ -750,24 +830,23 @@ static int c_light_accepts(const c_ctx* C, fv o, fv d) {
   const c_prim* P;
   if (l < 0 || l >= C->n) return 0;
   P = &C->prims[l];
-  if (P->kind == SPT_SPHERE) {
-    const float tt = P->wide ? c_sphere_wide(P, o, d) : c_sphere(P, o, d);
-    return tt != 0.0f && tt < 1e20f;
-  }
+  if (P->kind == SPT_SPHERE)
+    return c_key(P->wide ? c_sphere_wide(P, o, d) : c_sphere(P, o, d), C->light_pos) < C_KEY_NONE;
   {
-    float oa, da, tt, a, b;
+    float oa, da, tt, tb, a, b;
     switch (P->kind) {
       case SPT_RECT_XY: oa = o.z; da = d.z; break;
       case SPT_RECT_XZ: oa = o.y; da = d.y; break;
       default: oa = o.x; da = d.x; break;
     }
     tt = (P->k - oa) * spt_oracle_rcp_nr(da);
+    tb = asf(asu(tt) - 1u); /* the in-plane test at t- (contract v5, c_intersect) */
     switch (P->kind) {
-      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.y, tt, o.y - P->mb); break;
-      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
-      default: a = fmaf(d.y, tt, o.y - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
+      case SPT_RECT_XY: a = fmaf(d.x, tb, o.x - P->ma); b = fmaf(d.y, tb, o.y - P->mb); break;
+      case SPT_RECT_XZ: a = fmaf(d.x, tb, o.x - P->ma); b = fmaf(d.z, tb, o.z - P->mb); break;
+      default: a = fmaf(d.y, tb, o.y - P->ma); b = fmaf(d.z, tb, o.z - P->mb); break;
     }
-    return fabsf(a) <= P->ha && fabsf(b) <= P->hb && (asu(tt) - 1u) < (asu(1e20f) - 1u);
+    return fabsf(a) <= P->ha && fabsf(b) <= P->hb && c_key(tt, C->light_pos) < C_KEY_NONE;
   }
 }
 
@@ -780,9 +859,9 @@ static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0
 static float g_proof_y0;
 static uint64_t g_proof_n, g_proof_bad;
 static int c_early_nee_proven(fv o, fv d, float* tl) {
-  const float tt = (81.5f - o.y) * spt_oracle_rcp_nr(d.y);
-  const float a = fmaf(d.x, tt, o.x - 50.0f), b = fmaf(d.z, tt, o.z - 79.5f);
-  const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && (asu(tt) - 1u) < (asu(1e20f) - 1u);
+  const float tt = (81.5f - o.y) * spt_oracle_rcp_nr(d.y), tb = asf(asu(tt) - 1u);
+  const float a = fmaf(d.x, tb, o.x - 50.0f), b = fmaf(d.z, tb, o.z - 79.5f);
+  const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && c_key(tt, 8) < C_KEY_NONE;
   const int room = asu(o.x) - asu(1.0f) <= asu(99.0f) - asu(1.0f) && asu(o.z) <= asu(170.0f) &&
                    asu(o.y) < asu(81.5f);
   const int short_box = o.y > 25.0f || (o.x < 62.99f && a < 12.99f);
@@ -801,59 +880,95 @@ void spt_oracle_proof_counts(uint64_t out[2]) {
   out[1] = g_proof_bad;
 }
 
+/* Contract v5 (round 4). Every candidate is ranked by its key (c_key) and the nearest hit is the
+ * smallest key:
+ *  - a rect test gives one key per plane, t = (k - o_a) * inv_a; a parallel PAIR's candidate is
+ *    the smaller of its two planes' keys -- the smaller positive t, which is exactly the plane the
+ *    rounds-1-4 pair rule chose (the one ahead and nearer; the planes of a pair are >= 25 units
+ *    apart, far more than the keys' 64 ulps) -- and its in-plane test is evaluated at
+ *    t- = float(min(bits(t0) - 1, bits(t1) - 1)), the float just below the chosen t; a single's at
+ *    float(bits(t) - 1). Accepted iff |a| <= half and |b| <= half there (:104-106);
+ *  - the ROOM (c_find_room) is one box: the smallest of its three pairs' keys is the candidate, and
+ *    it is accepted iff its point at t_R = float(key) lies in the room box widened by 2^-8 on every
+ *    axis. For an origin in the room the nearest of the three exit planes always lies in the box
+ *    (the box is convex); the test only rejects origins outside (a leaked path), where a ray that
+ *    enters the box is accepted at its entry plane and one that passes by is not. It differs from
+ *    the per-wall test only within 2^-8 of a room edge (and for origins outside two of the three
+ *    slabs at once), and it replaces six bounds compares by three;
+ *  - spheres: key(t, position) of the nearest root beyond the epsilon (0 = no root, ranked last).
+ * The hit's t is the winner's own t, recomputed from its plane / sphere (the same bits as in its
+ * key). id is left untouched on a miss; returns 1 on hit, *t = 1e20f on a miss. */
 static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   const float ix = spt_oracle_rcp_nr(d.x), iy = spt_oracle_rcp_nr(d.y), iz = spt_oracle_rcp_nr(d.z);
-  float tmin = 1e20f;
-  int i;
+  uint32_t tmin = C_KEY_NONE;
+  int i, pos;
   for (i = 0; i < C->n_tests; i++) {
     const c_test* T = &C->tests[i];
-    float oa, ia, tt, a, b, n0, n1;
-    int sel1;
+    float oa, ia, tb, a, b;
+    uint32_t kp;
+    const int room = i == C->room[0] || i == C->room[1] || i == C->room[2];
     switch (T->kind) {
       case SPT_RECT_XY: oa = o.z; ia = iz; break;
       case SPT_RECT_XZ: oa = o.y; ia = iy; break;
       default: oa = o.x; ia = ix; break;
     }
-    n0 = T->k0 - oa;
-    n1 = T->k1 - oa;
-    sel1 = ia > 0.0f ? !(n0 > 0.0f) : (n1 < 0.0f);
-    tt = (sel1 ? n1 : n0) * ia;
-    /* In-plane offsets from the rectangle's centre: a = d_b * t + (o_b - mid_b) in one fma (the
-     * origin's offset o_b - mid_b is per ray, shared by every rectangle with that centre). */
-    switch (T->kind) {
-      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x - T->ma); b = fmaf(d.y, tt, o.y - T->mb); break;
-      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x - T->ma); b = fmaf(d.z, tt, o.z - T->mb); break;
-      default: a = fmaf(d.y, tt, o.y - T->ma); b = fmaf(d.z, tt, o.z - T->mb); break;
-    }
-    /* :106 rejects x<x1||x>x2||z<z1||z>z2||t<0 and :328 needs t != 0 && t < tmin:
-     * bounds as |a| <= half per axis (c_rect_mid), 0 < t < tmin as one unsigned compare of the
-     * float bit patterns minus one (exact for every float incl. +-0, inf, NaN). */
+    if (room) continue; /* below */
     {
-      const int inb = fabsf(a) <= T->ha && fabsf(b) <= T->hb;
-      const int trange = (asu(tt) - 1u) < (asu(tmin) - 1u);
-      if (inb && trange) {
-        tmin = tt;
-        *id = sel1 ? T->id1 : T->id0;
+      const float t0 = (T->k0 - oa) * ia;
+      if (T->id0 != T->id1) {
+        const float t1 = (T->k1 - oa) * ia;
+        kp = c_umin(c_key(t0, T->pos0), c_key(t1, T->pos1));
+        tb = asf(c_umin(asu(t0) - 1u, asu(t1) - 1u));
+      } else {
+        kp = c_key(t0, T->pos0);
+        tb = asf(asu(t0) - 1u);
       }
     }
+    /* in-plane offsets from the rectangle's centre, a = d_b * t + (o_b - mid_b) in one fma */
+    switch (T->kind) {
+      case SPT_RECT_XY: a = fmaf(d.x, tb, o.x - T->ma); b = fmaf(d.y, tb, o.y - T->mb); break;
+      case SPT_RECT_XZ: a = fmaf(d.x, tb, o.x - T->ma); b = fmaf(d.z, tb, o.z - T->mb); break;
+      default: a = fmaf(d.y, tb, o.y - T->ma); b = fmaf(d.z, tb, o.z - T->mb); break;
+    }
+    if (fabsf(a) <= T->ha && fabsf(b) <= T->hb) tmin = c_umin(tmin, kp);
   }
-  /* Spheres in index order, the narrow (fp32) ones first, then the wide (fp64) ones. */
-  for (i = 0; i < 2 * C->n; i++) {
-    const int k = i % C->n;
-    const c_prim* P = &C->prims[k];
-    if (P->kind != SPT_SPHERE || P->wide != (i >= C->n)) continue;
-    if (P->wide) {
-      const float tt = c_sphere_wide(P, o, d);
-      if (tt != 0.0f && tt < tmin) { tmin = tt; *id = k; }
-      continue;
+  if (C->room[0] >= 0) {
+    uint32_t rk = 0xFFFFFFFFu;
+    int r;
+    for (r = 0; r < 3; r++) {
+      const c_test* T = &C->tests[C->room[r]];
+      const float oa = r == 0 ? o.z : (r == 1 ? o.y : o.x), ia = r == 0 ? iz : (r == 1 ? iy : ix);
+      rk = c_umin(rk, c_umin(c_key((T->k0 - oa) * ia, T->pos0), c_key((T->k1 - oa) * ia, T->pos1)));
     }
     {
-      const float tt = c_sphere(P, o, d);
-      if (tt != 0.0f && tt < tmin) { tmin = tt; *id = k; }
+      const float tr = asf(rk);
+      const float ax = fmaf(d.x, tr, o.x - C->room_m[0]), ay = fmaf(d.y, tr, o.y - C->room_m[1]),
+                  az = fmaf(d.z, tr, o.z - C->room_m[2]);
+      if (fabsf(ax) <= C->room_h[0] && fabsf(ay) <= C->room_h[1] && fabsf(az) <= C->room_h[2])
+        tmin = c_umin(tmin, rk);
     }
   }
-  *t = tmin;
-  return tmin < 1e20f;
+  /* Spheres: narrow (fp32) ones, then the wide (fp64) ones, each in index order (their positions) */
+  for (i = C->n_rect; i < C->n; i++) {
+    const c_prim* P = &C->prims[C->pos2idx[i]];
+    tmin = c_umin(tmin, c_key(P->wide ? c_sphere_wide(P, o, d) : c_sphere(P, o, d), i));
+  }
+  if (!(tmin < C_KEY_NONE)) {
+    *t = 1e20f;
+    return 0;
+  }
+  pos = (int)(tmin & 63u);
+  *id = C->pos2idx[pos];
+  {
+    const c_prim* H = &C->prims[*id];
+    switch (H->kind) {
+      case SPT_RECT_XY: *t = (H->k - o.z) * iz; break;
+      case SPT_RECT_XZ: *t = (H->k - o.y) * iy; break;
+      case SPT_RECT_YZ: *t = (H->k - o.x) * ix; break;
+      default: *t = H->wide ? c_sphere_wide(H, o, d) : c_sphere(H, o, d);
+    }
+  }
+  return 1;
 }
 
 /* random_scattering in the contract: cosine (:340-347), or with `uniform` the commented-out
@@ -945,6 +1060,20 @@ typedef struct {
   uint32_t branch;
 } c_node;
 
+/* light_sampling :365-366 as built with glibc: x0 + rand()*dx/RAND_MAX with rand()*dx computed in
+ * int32, which wraps. For dx = 2^a * odd (1 <= a <= 24) the wrapped product of
+ * a uniform draw is uniform on the 2^(25-a) points x0 - 1 + m 2^(a-24), m in [0, 2^(25-a)) (an odd
+ * factor permutes the residues), so contract v5 takes m from the top 25 - a bits of the Philox word:
+ * fma(m, 2^(a-24), x0 - 1). (Rounds 1-4 multiplied a 24-bit draw by 2^7 dx and wrapped it: the same
+ * lattice, points drawn in another order; the GPU's HEAD kernel now builds the float from the bits
+ * with one or, dx = 36 = 4 * 9.) Odd dx keeps the rounds-1-4 arithmetic. */
+static float c_wrap_sample(uint32_t r, uint32_t dx, float x0) {
+  int a = 0;
+  while (a < 32 && dx != 0 && !((dx >> a) & 1u)) a++;
+  if (dx != 0 && a >= 1 && a <= 24) return fmaf((float)(r >> (7 + a)), ldexpf(1.0f, a - 24), x0 - 1.0f);
+  return fmaf((float)(int32_t)(((r >> 8) << 7) * dx), 0x1p-31f, x0);
+}
+
 /* One path of the counter-mode contract; returns L. */
 static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const float cam[12],
                  c_stats* st) {
@@ -960,13 +1089,26 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
   ctr[0] = pix; ctr[1] = s; ctr[2] = 1; ctr[3] = P->seed;
   c_philox(ctr, C->key, r);
   {
+    /* Contract v5: d = llc + hor*su + ver*sv - origin with su = (x - 0.5 + ju 2^-16) / w,
+     * sv = (h - y - 1 - 0.5 + jv 2^-16) / h (:533-536) as, per component c,
+     *   fma(Fv, Cv_c, fma(Fu, Cu_c, P_c)),  Fu = 2^23 + ju, Fv = 2^23 + jv (exact floats),
+     *   Au_c = hor_c * (1/w), Av_c = ver_c * (1/h), Cu_c = Au_c 2^-16, Cv_c = Av_c 2^-16,
+     *   P_c = fma(Au_c, fx, fma(Av_c, fy, llc_c - origin_c)), fx = x - 0.5 - 128, fy = h-y-1-0.5 - 128
+     * (the -128 cancels the 2^23 2^-16 = 128 inside Fu * Cu). P_c is per pixel: on the GPU a camera
+     * ray costs one fma per component after the jitter bits (rounds 1-4: jitter, scale, fma chain,
+     * subtract). */
     const float inv_w = 1.0f / (float)P->width, inv_h = 1.0f / (float)P->height;
-    const float su = (((float)px - 0.5f) + u16(r[0], r[1])) * inv_w;
-    const float sv = (((float)(P->height - py - 1) - 0.5f) + u16(r[2], r[3])) * inv_h;
+    const float fx = ((float)px - 0.5f) - 128.0f, fy = ((float)(P->height - py - 1) - 0.5f) - 128.0f;
+    const float Fu = asf(0x4B000000u | u16i(r[0], r[1])), Fv = asf(0x4B000000u | u16i(r[2], r[3]));
+    float v[3];
+    int c;
+    for (c = 0; c < 3; c++) {
+      const float Au = cam[6 + c] * inv_w, Av = cam[9 + c] * inv_h;
+      const float Pc = fmaf(Au, fx, fmaf(Av, fy, cam[3 + c] - cam[c]));
+      v[c] = fmaf(Fv, Av * 0x1p-16f, fmaf(Fu, Au * 0x1p-16f, Pc));
+    }
     o = fv3(cam[0], cam[1], cam[2]);
-    d = fv3(fmaf(cam[9], sv, fmaf(cam[6], su, cam[3])) - cam[0],
-            fmaf(cam[10], sv, fmaf(cam[7], su, cam[4])) - cam[1],
-            fmaf(cam[11], sv, fmaf(cam[8], su, cam[5])) - cam[2]);
+    d = fv3(v[0], v[1], v[2]);
     d = C->unit ? fnormalize(d) : fnormalize2(d);
   }
   st->samples++;
@@ -1098,10 +1240,8 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         int ids = id, sh;
         fv dl;
         if (P->light_mode == SPT_LIGHT_GLIBC_WRAP) {
-          const uint32_t dxi = (uint32_t)P->light_dx, dzi = (uint32_t)P->light_dz;
-          /* rand()*36 in int32 (:365): a 31-bit draw (top 24 bits, low 7 zero) times dx, wrapped */
-          xl = fmaf((float)(int32_t)(((r[0] >> 8) << 7) * dxi), 0x1p-31f, P->light_x0);
-          zl = fmaf((float)(int32_t)(((r[1] >> 8) << 7) * dzi), 0x1p-31f, P->light_z0);
+          xl = c_wrap_sample(r[0], (uint32_t)P->light_dx, P->light_x0);
+          zl = c_wrap_sample(r[1], (uint32_t)P->light_dz, P->light_z0);
         } else {
           xl = fmaf(u01(r[0]), P->light_dx, P->light_x0);
           zl = fmaf(u01(r[1]), P->light_dz, P->light_z0);

@@ -9,7 +9,11 @@
 
 namespace spt {
 
-struct CRect { float k, ma, ha, mb, hb; int idx; };
+struct CRect {
+  float k, ma, ha, mb, hb;
+  int idx;
+  double a1, a2, b1, b2, kd;  // the constructor's doubles (the room rule compares them exactly)
+};
 
 constexpr double pow2i(int e) {
   double r = 1;
@@ -53,7 +57,8 @@ static_assert(plane_k(81.6) == 81.600006103515625f && plane_k(81.5) == 81.5f &&
 // Same rounding as build_geo()/rect_mid() on the host: bounds rounded once from double.
 constexpr CRect crect(double a1, double a2, double b1, double b2, double k, int idx) {
   return CRect{plane_k(k), (float)((a1 + a2) * 0.5), a2 >= a1 ? (float)((a2 - a1) * 0.5) : -1.0f,
-               (float)((b1 + b2) * 0.5), b2 >= b1 ? (float)((b2 - b1) * 0.5) : -1.0f, idx};
+               (float)((b1 + b2) * 0.5), b2 >= b1 ? (float)((b2 - b1) * 0.5) : -1.0f, idx,
+               a1, a2, b1, b2, k};
 }
 
 // Rectangle_xy(x1,x2,y1,y2,z) :97-98; Rectangle_xz(x1,x2,z1,z2,y) :142; Rectangle_yz(y1,y2,z1,z2,x) :185
@@ -105,5 +110,49 @@ constexpr CTestList cornell_tests() {
 }
 constexpr CTestList kCornellTests = cornell_tests();
 static_assert(kCornellTests.n == 10, "HEAD scene: 7 parallel pairs + light + 2 box tops");
+
+// The room of contract v5 (oracle c_find_room): the first XY, XZ, YZ pair tests (in test order)
+// whose planes are exactly the other pairs' in-plane bounds. HEAD: Front/Back, Bottom/Top,
+// Left/Right (:288-293).
+constexpr bool same_range(double k1, double k2, double b1, double b2) {
+  return (k1 < k2 ? k1 : k2) == b1 && (k1 < k2 ? k2 : k1) == b2;
+}
+struct CRoom { int t[3]; float box[6]; };  // tests (XY, XZ, YZ); mid, half + 2^-8 for x, y, z
+constexpr CRoom cornell_room() {
+  CRoom R{{-1, -1, -1}, {}};
+  const CTestList& L = kCornellTests;
+  for (int a = 0; a < L.n; ++a) {
+    if (L.t[a].axis != 2 || L.t[a].pos0 == L.t[a].pos1) continue;
+    for (int b = 0; b < L.n; ++b) {
+      if (L.t[b].axis != 1 || L.t[b].pos0 == L.t[b].pos1) continue;
+      for (int c = 0; c < L.n; ++c) {
+        if (L.t[c].axis != 0 || L.t[c].pos0 == L.t[c].pos1) continue;
+        const CRect& A0 = kCornellRects[L.t[a].pos0];  // XY: bounds x, y; planes z
+        const CRect& A1 = kCornellRects[L.t[a].pos1];
+        const CRect& B0 = kCornellRects[L.t[b].pos0];  // XZ: bounds x, z; planes y
+        const CRect& B1 = kCornellRects[L.t[b].pos1];
+        const CRect& D0 = kCornellRects[L.t[c].pos0];  // YZ: bounds y, z; planes x
+        const CRect& D1 = kCornellRects[L.t[c].pos1];
+        // bounds from each pair's k0 member (the oracle's c_test.id0)
+        if (!same_range(D0.kd, D1.kd, A0.a1, A0.a2) || !same_range(D0.kd, D1.kd, B0.a1, B0.a2) ||
+            !same_range(B0.kd, B1.kd, A0.b1, A0.b2) || !same_range(B0.kd, B1.kd, D0.a1, D0.a2) ||
+            !same_range(A0.kd, A1.kd, B0.b1, B0.b2) || !same_range(A0.kd, A1.kd, D0.b1, D0.b2))
+          continue;
+        R.t[0] = a; R.t[1] = b; R.t[2] = c;
+        R.box[0] = A0.ma; R.box[1] = A0.ha + 0x1p-8f;
+        R.box[2] = A0.mb; R.box[3] = A0.hb + 0x1p-8f;
+        R.box[4] = B0.mb; R.box[5] = B0.hb + 0x1p-8f;
+        return R;
+      }
+    }
+  }
+  return R;
+}
+constexpr CRoom kCornellRoomDef = cornell_room();
+constexpr int kCornellRoom[3] = {kCornellRoomDef.t[0], kCornellRoomDef.t[1], kCornellRoomDef.t[2]};
+static_assert(kCornellRoom[0] == 0 && kCornellRoom[1] == 3 && kCornellRoom[2] == 7,
+              "HEAD room: Front/Back, Bottom/Top, Left/Right");
+static_assert(kCornellRoomDef.box[0] == 50.0f && kCornellRoomDef.box[1] == 49.0f + 0x1p-8f &&
+                  kCornellRoomDef.box[5] == 85.0f + 0x1p-8f, "HEAD room box");
 
 }  // namespace spt

@@ -91,7 +91,10 @@ __device__ __forceinline__ u4 philox_px(PxKey pk, uint32_t c1, uint32_t c2) {
   return u4{c0, c1, c2, c3};
 }
 
-__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
+// A uniform [0, 1) float from the top 23 bits (contract v5, oracle u01): the float 1 + m 2^-23
+// (bits 0x3F800000 | m) minus 1 -- an or and a subtract (rounds 1-4: shift, half-rate conversion,
+// multiply)
+__device__ __forceinline__ float u01(uint32_t v) { return __uint_as_float(0x3F800000u | (v >> 9)) - 1.0f; }
 // 16-bit draw from the low bytes of two Philox words (RR and NEE-mix draws, camera jitter; see
 // the kernel): (lo & 0xFF) | (hi & 0xFF) << 8 as ONE v_perm_b32 (bytes {hi:lo}[4], [0], 0, 0).
 __device__ __forceinline__ uint32_t u16i(uint32_t lo, uint32_t hi) {

@@ -135,10 +135,14 @@ struct GeoTest { float k0, k1, ma, ha, mb, hb; int pos0, pos1; };      // 32 B
 struct SceneGeo {
   int n_xy, n_xz, n_yz, n_sph;
   int n_txy, n_txz, n_tyz, n_sph_wide;  // rect tests per kind; wide spheres = the last n_sph_wide
+  // contract v5's room (oracle c_find_room): its three pair tests follow the per-kind lists in
+  // test[] (XY, XZ, YZ); box = mid, half + 2^-8 for x, y, z
+  int has_room, pad_[3];
+  float room_box[6], pad2_[2];
   GeoRect rect[kMaxPrims];  // [0,n_xy) XY, [n_xy, n_xy+n_xz) XZ, then YZ
   GeoSph sph[kMaxPrims];
   GeoSphD sphd[kMaxPrims];
-  GeoTest test[kMaxPrims];  // [0,n_txy) XY, then XZ, then YZ
+  GeoTest test[kMaxPrims];  // [0,n_txy) XY, then XZ, then YZ (room tests excluded), then the room
 };
 #define SPT_CONST __attribute__((address_space(4)))
 
@@ -167,6 +171,13 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   uint32_t scr_k, scr_q;  // pixel-order spreading of the units: K = 2^scr_k, scr_q = npix / K
   float inv_spp, inv_w, inv_h;
   float fix_scale;  // inv_spp * 2^31 (fix31)
+  // camera of contract v5 (jitter_f): Au, Av, Cu = Au 2^-16, Cv = Av 2^-16, L = llc - origin per axis
+  float cam_au[3], cam_av[3], cam_cu[3], cam_cv[3], cam_l[3];
+  // light sample of contract v5 (oracle c_wrap_sample): GLIBC_WRAP with dx = 2^a odd, 1 <= a <= 24:
+  // x0 - 1 + (r >> (7 + a)) 2^(a - 24); else (lattice 0) the rounds-1-4 wrapped multiply
+  int lx_lattice, lz_lattice;
+  uint32_t lx_shift, lz_shift;
+  float lx_scale, lz_scale, lx0m1, lz0m1;
   // Shadow-ray specialisation: when the light is black (c == 0, HEAD :294) a path that reaches it
   // always ends there (RR with p == 0, :448), so the NEE test only needs "is the nearest hit the
   // light" — an occlusion query without id bookkeeping.
@@ -191,12 +202,6 @@ __device__ __forceinline__ const SPT_CONST T* cptr(const T* p) {
   return (const SPT_CONST T*)p;
 }
 
-// Scene intersection of the counter-mode contract (intersect :323-335 over Rectangle_* :102-112 /
-// Sphere :229-239): grouped kind order, strict `<`, id untouched on a miss (oracle c_intersect).
-// tmin is carried as key = bits(t) - 1 so "0 < t < tmin" is ONE unsigned compare; the hit is
-// tracked as its grouped position (an inline constant when unrolled) and mapped to the primitive
-// index through LDS once per ray.
-__device__ __forceinline__ uint32_t tkey(float t) { return __float_as_uint(t) - 1u; }
 
 // Rect geometry with literal operands: kCornellRects[i] at a compile-time i (spt_cornell.h).
 struct CornellRectPtr {
@@ -223,9 +228,9 @@ struct Topo {
   // -1 = KParams::unit_dirs at run time (the generic kernels)
   static constexpr int DIRS = MAT_ ? -1 : (SPH_ ? 1 : 0);
 };
-// rect[] of :287-311 (light = XZ #3 -> pos 8); tests: 3 XY pairs, XZ floor/ceiling pair + light +
-// 2 box tops, 3 YZ pairs
-using TopoCornell = Topo<6, 5, 6, false, 8, false, 3, 4, 3>;
+// rect[] of :287-311 (light = XZ #3 -> pos 8); tests besides the room (contract v5): 2 XY box
+// pairs; light + 2 box tops; 2 YZ box pairs
+using TopoCornell = Topo<6, 5, 6, false, 8, false, 2, 3, 2>;
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 // Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
@@ -296,115 +301,123 @@ __device__ __forceinline__ Ray6 ray6(f3 o, f3 d, float ix, float iy, float iz) {
   return Ray6{o.x, ix, d.y, o.y, d.z, o.z};
 }
 
-// One rect test of the contract (oracle c_intersect). A parallel pair tests the plane that can be
-// hit first: k0 when the ray moves up the axis (inv_a > 0) from below it (n0 > 0) or down the axis
-// from anywhere not above k1 (n1 >= 0), else k1; t = n * inv_a as for a single rectangle.
-// v_cndmask with an explicit 64-bit lane mask: LLVM turns the pair rule's mask logic into a select
-// of booleans held in VGPRs (~6 VALU); as SALU operations on ballot masks it is free.
-__device__ __forceinline__ float sel_f(uint64_t m, float a, float b) {  // m ? b : a per lane
-  float r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+// ---- Nearest hit, contract v5 (round 4; oracle c_intersect / c_key). A candidate at t on the plane
+// or sphere with grouped position pos is ranked by its KEY: the bits of t minus one (so 0 < t < tmin
+// stays one unsigned compare; +-0, negatives, inf and NaN rank last) with the low 6 bits replaced
+// by pos; the nearest hit is the smallest key. Per candidate that is one v_add, one v_bitop3 and
+// one v_min_u32 -- where rounds 1-4 compared keys and selected (t, position) through lane masks,
+// a v_cmp -> s_and -> two v_cndmask chain per test: C3 13.56 -> 12.92 ms (A/B, profiles/r04_ab.txt).
+// A parallel pair's candidate is the smaller of its two planes' keys (the smaller positive t: the
+// plane the rounds-1-4 pair rule chose); its in-plane test is evaluated at t- = the float below the
+// chosen t. The winner's exact t is recomputed by whoever needs it (shading, NEE weight) from its
+// plane or sphere: the same bits as in its key.
+constexpr uint32_t kKeyNone = (__builtin_bit_cast(uint32_t, 1e20f) - 1u) | 63u;  // tmin = 1e20 (:324)
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// ((bits(t) - 1) | 63) ^ (63 - pos) as ONE v_bitop3 (0x36 = (S0 | S2) ^ S1) after the v_add
+template <int POS>
+__device__ __forceinline__ uint32_t key_c(float t) {  // compile-time position (inline constant)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t) - 1u), "n"(63 - POS));
   return r;
 }
-__device__ __forceinline__ int sel_i(uint64_t m, int a, int b) {
-  int r;
-  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+__device__ __forceinline__ uint32_t key_v(float t, uint32_t pos) {  // position in a VGPR
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t) - 1u), "v"(63u - pos));
   return r;
 }
-template <int A, int B>  // compile-time positions as inline constants
-__device__ __forceinline__ int sel_ic(uint64_t m) {
-  int r;
-  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "I"(A), "I"(B), "s"(m));
+__device__ __forceinline__ uint32_t key_s(float t, uint32_t pos) {  // wave-uniform position (SGPR)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t) - 1u), "s"(63u - pos));
   return r;
-}
-// Grouped position of the tested plane of a pair.
-struct GeoTest;
-template <int J> struct CornellTestPtr;
-template <int J>
-__device__ __forceinline__ int pair_pos(CornellTestPtr<J>, uint64_t sel1);
-__device__ __forceinline__ int pair_pos(const SPT_CONST GeoTest* g, uint64_t sel1);
-__device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
-
-// One rect test of the contract (oracle c_intersect). A parallel pair tests the plane that can be
-// hit first: k0 when the ray moves up the axis (inv_a > 0) from below it (n0 > 0) or down the axis
-// from anywhere not above k1 (n1 >= 0), else k1; t = n * inv_a as for a single rectangle.
-// up: lane mask of inv_a > 0.
-template <bool PAIR, class GP>
-__device__ __forceinline__ void rect_test(GP g, const Ray6& r, uint64_t up, uint32_t& tmin_key,
-                                          int& pos) {
-  const float n0 = g->k0 - r.oa;
-  float n = n0;
-  uint64_t sel1 = 0;
-  if constexpr (PAIR) {
-    const float n1 = g->k1 - r.oa;
-    // sel1 = up ? !(n0 > 0) : (n1 < 0) (oracle c_intersect) as ONE compare and one SALU xor:
-    // z = up ? n0 : -n1, sel1 = (z > 0) ^ up -- exact for every n0, n1 (NaN and signed zeros incl.)
-    const float z = (r.ia > 0.0f) ? n0 : -n1;
-    sel1 = lanes(z > 0.0f) ^ up;
-    n = sel_f(sel1, n0, n1);
-  }
-  const float tt = n * r.ia;
-  // in-plane offsets from the centre, a = d_b * t + (o_b - mid_b): the origin's offset is per ray
-  // and shared by every rectangle with that centre (CSE'd across the unrolled tests)
-  const float a = fmaf(r.db, tt, r.ob - g->ma), b = fmaf(r.dc, tt, r.oc - g->mb);
-  const bool inb = (bool)((int)(fabsf(a) <= g->ha) & (int)(fabsf(b) <= g->hb));
-  const uint32_t kk = tkey(tt);
-  const bool acc = inb & (kk < tmin_key);
-  tmin_key = acc ? kk : tmin_key;
-  if constexpr (PAIR) {
-    const int q = pair_pos(g, sel1);
-    pos = acc ? q : pos;
-  }
-  else pos = acc ? g->pos0 : pos;
 }
 
-// Compile-time HEAD tests (spt_cornell.h kCornellTests): every operand a literal.
-template <int J>
-struct CornellTestPtr {
+// One rect test (oracle c_intersect): a single (k0 == k1) or a parallel pair. KEYS: the per-plane
+// key function for compile-time (CornellTestPtr) or LDS/scalar (GeoTest) geometry.
+template <int J> struct CornellTestPtr {
   __device__ constexpr const CTest* operator->() const { return &kCornellTests.t[J]; }
 };
+template <int J, bool PAIR>
+__device__ __forceinline__ void plane_keys(CornellTestPtr<J>, float t0, float t1, uint32_t& kp) {
+  if constexpr (PAIR) kp = umin(key_c<kCornellTests.t[J].pos0>(t0), key_c<kCornellTests.t[J].pos1>(t1));
+  else kp = key_c<kCornellTests.t[J].pos0>(t0);
+}
+template <int J, bool PAIR>  // (unused J: a runtime pointer)
+__device__ __forceinline__ void plane_keys(const GeoTest* g, float t0, float t1, uint32_t& kp) {
+  kp = umin(key_v(t0, (uint32_t)g->pos0), key_v(t1, (uint32_t)g->pos1));
+}
+template <int J, bool PAIR>
+__device__ __forceinline__ void plane_keys(const SPT_CONST GeoTest* g, float t0, float t1, uint32_t& kp) {
+  kp = umin(key_v(t0, (uint32_t)g->pos0), key_v(t1, (uint32_t)g->pos1));
+}
+template <int J, bool PAIR, class GP>
+__device__ __forceinline__ void rect_cand(GP g, const Ray6& r, uint32_t& tmin) {
+  const float t0 = (g->k0 - r.oa) * r.ia;
+  float t1 = t0;
+  uint32_t kb = __float_as_uint(t0) - 1u, kp;
+  if constexpr (PAIR) {
+    t1 = (g->k1 - r.oa) * r.ia;
+    kb = umin(kb, __float_as_uint(t1) - 1u);
+  }
+  plane_keys<J, PAIR>(g, t0, t1, kp);
+  const float tb = __uint_as_float(kb);  // t- of the chosen plane
+  // in-plane offsets from the centre, a = d_b * t + (o_b - mid_b): the origin's offset is per ray
+  // and shared by every rectangle with that centre (CSE'd across the unrolled tests)
+  const float a = fmaf(r.db, tb, r.ob - g->ma), b = fmaf(r.dc, tb, r.oc - g->mb);
+  const bool inb = (bool)((int)(fabsf(a) <= g->ha) & (int)(fabsf(b) <= g->hb));
+  tmin = umin(tmin, inb ? kp : 0xFFFFFFFFu);
+}
+// The room's pair (oracle c_intersect, the room): the smaller key of its two planes, no bounds.
+template <int J, class GP>
+__device__ __forceinline__ uint32_t room_pair(GP g, const Ray6& r) {
+  const float t0 = (g->k0 - r.oa) * r.ia, t1 = (g->k1 - r.oa) * r.ia;
+  uint32_t kp;
+  plane_keys<J, true>(g, t0, t1, kp);
+  return kp;
+}
+// The room as one box: the nearest of its three pairs, accepted iff the point at t_R = float(key)
+// lies in the room box widened by 2^-8 (mid m, half h + 2^-8 per axis x, y, z).
+__device__ __forceinline__ void room_accept(uint32_t rk, f3 o, f3 d, float mx, float hx, float my,
+                                            float hy, float mz, float hz, uint32_t& tmin) {
+  const float tr = __uint_as_float(rk);
+  const float ax = fmaf(d.x, tr, o.x - mx), ay = fmaf(d.y, tr, o.y - my), az = fmaf(d.z, tr, o.z - mz);
+  const bool inb = (bool)((int)(fabsf(ax) <= hx) & (int)(fabsf(ay) <= hy) & (int)(fabsf(az) <= hz));
+  tmin = umin(tmin, inb ? rk : 0xFFFFFFFFu);
+}
 template <int J>
-__device__ __forceinline__ int pair_pos(CornellTestPtr<J>, uint64_t sel1) {
-  return sel_ic<kCornellTests.t[J].pos0, kCornellTests.t[J].pos1>(sel1);
-}
-__device__ __forceinline__ int pair_pos(const SPT_CONST GeoTest* g, uint64_t sel1) {
-  return sel_i(sel1, g->pos0, g->pos1);
-}
-__device__ __forceinline__ int pair_pos(const GeoTest* g, uint64_t sel1) {  // LDS copy (A/B)
-  return sel_i(sel1, g->pos0, g->pos1);
-}
-template <int J>
-__device__ __forceinline__ void cornell_test(const Ray6* rays, const uint64_t* up, uint32_t& tmin_key,
-                                             int& pos) {
-  constexpr int ax = kCornellTests.t[J].axis;
-  constexpr bool pair = kCornellTests.t[J].pos0 != kCornellTests.t[J].pos1;
-  rect_test<pair>(CornellTestPtr<J>{}, rays[ax], up[ax], tmin_key, pos);
+__device__ __forceinline__ void cornell_test(const Ray6* rays, uint32_t& tmin) {
+  constexpr CTest T = kCornellTests.t[J];
+  if constexpr (J != kCornellRoom[0] && J != kCornellRoom[1] && J != kCornellRoom[2])
+    rect_cand<J, T.pos0 != T.pos1>(CornellTestPtr<J>{}, rays[T.axis], tmin);
 }
 template <int... J>
 __device__ __forceinline__ void cornell_tests(std::integer_sequence<int, J...>, const Ray6* rays,
-                                              const uint64_t* up, uint32_t& tmin_key, int& pos) {
-  (cornell_test<J>(rays, up, tmin_key, pos), ...);
+                                              uint32_t& tmin) {
+  (cornell_test<J>(rays, tmin), ...);
 }
 
 template <int N, class GT>  // the tests of one kind group, uploaded geometry (every test as a pair)
-__device__ __forceinline__ void test_group(GT g, int n_rt, const Ray6& r, uint32_t& tmin_key,
-                                           int& pos) {
-  const uint64_t up = lanes(r.ia > 0.0f);
+__device__ __forceinline__ void test_group(GT g, int n_rt, const Ray6& r, uint32_t& tmin) {
   if constexpr (N >= 0) {
 #pragma unroll
-    for (int j = 0; j < N; ++j) rect_test<true>(g + j, r, up, tmin_key, pos);
+    for (int j = 0; j < N; ++j) rect_cand<0, true>(g + j, r, tmin);
   } else {
-    for (int j = 0; j < n_rt; ++j) rect_test<true>(g + j, r, up, tmin_key, pos);
+    for (int j = 0; j < n_rt; ++j) rect_cand<0, true>(g + j, r, tmin);
   }
 }
 
+// One rectangle's own test (a single, as inside the trace: contract v5): t, whether its in-plane
+// test at t- accepts, and the first in-plane offset there.
 struct RectHit { float tt; bool inb; float a; };  // a: first in-plane offset from the centre
 template <class GP>
 __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
-  const float tt = (g->k - r.oa) * r.ia;
-  const float a = fmaf(r.db, tt, r.ob - g->ma), b = fmaf(r.dc, tt, r.oc - g->mb);
+  const float tt = (g->k - r.oa) * r.ia, tb = __uint_as_float(__float_as_uint(tt) - 1u);
+  const float a = fmaf(r.db, tb, r.ob - g->ma), b = fmaf(r.dc, tb, r.oc - g->mb);
   const bool ia = fabsf(a) <= g->ha, ib = fabsf(b) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib), a};
+}
+// A candidate at t with position pos can be the nearest hit at all: its key ranks below "none".
+__device__ __forceinline__ bool key_valid(float t, uint32_t pos) {
+  return (((__float_as_uint(t) - 1u) | 63u) ^ (63u - pos)) < kKeyNone;
 }
 
 template <class SP>
@@ -472,24 +485,38 @@ __device__ __forceinline__ auto tests_of(const SPT_CONST SceneGeo* G, const GeoT
     return G->test + 0;
   }
 }
+// The scene's room of contract v5 in uploaded geometry: SceneGeo.room_test[] (three GeoTests kept
+// out of the per-kind test lists) and the box (host build_geo, oracle c_find_room).
 template <class TP, class GP, class GT, class SP>
 __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect, GT tests,
-                                                SP sphs, const int* pos2idx, f3 o, f3 d,
-                                                float& t_out, int& id, float& ia_hit) {
+                                                SP sphs, const int* pos2idx, f3 o, f3 d, int& id,
+                                                float& ia_hit, int& pos_out) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
-  uint32_t tmin_key = tkey(1e20f);
-  int pos = -1;
+  uint32_t tmin = kKeyNone;
   if constexpr (TP::CONSTGEO) {
     const Ray6 rays[3] = {ray6<0>(o, d, ix, iy, iz), ray6<1>(o, d, ix, iy, iz),
                           ray6<2>(o, d, ix, iy, iz)};
-    const uint64_t up[3] = {lanes(ix > 0.0f), lanes(iy > 0.0f), lanes(iz > 0.0f)};
-    cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, up, tmin_key, pos);
+    constexpr int R0 = kCornellRoom[0], R1 = kCornellRoom[1], R2 = kCornellRoom[2];
+    const uint32_t rk = umin(umin(room_pair<R0>(CornellTestPtr<R0>{}, rays[kCornellTests.t[R0].axis]),
+                                  room_pair<R1>(CornellTestPtr<R1>{}, rays[kCornellTests.t[R1].axis])),
+                             room_pair<R2>(CornellTestPtr<R2>{}, rays[kCornellTests.t[R2].axis]));
+    constexpr CRoom B = kCornellRoomDef;
+    room_accept(rk, o, d, B.box[0], B.box[1], B.box[2], B.box[3], B.box[4], B.box[5], tmin);
+    cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);
   } else {
     const int ntxy = n_of<TP>(TP::NTXY, G->n_txy), ntxz = n_of<TP>(TP::NTXZ, G->n_txz);
     const int ntyz = n_of<TP>(TP::NTYZ, G->n_tyz);
-    test_group<TP::NTXY>(tests, ntxy, ray6<2>(o, d, ix, iy, iz), tmin_key, pos);
-    test_group<TP::NTXZ>(tests + ntxy, ntxz, ray6<1>(o, d, ix, iy, iz), tmin_key, pos);
-    test_group<TP::NTYZ>(tests + ntxy + ntxz, ntyz, ray6<0>(o, d, ix, iy, iz), tmin_key, pos);
+    const Ray6 rz = ray6<2>(o, d, ix, iy, iz), ry = ray6<1>(o, d, ix, iy, iz), rx = ray6<0>(o, d, ix, iy, iz);
+    if (G->has_room) {  // wave-uniform; the room tests follow the per-kind lists
+      const int nt = ntxy + ntxz + ntyz;
+      const uint32_t rk = umin(umin(room_pair<0>(tests + nt, rz), room_pair<0>(tests + nt + 1, ry)),
+                               room_pair<0>(tests + nt + 2, rx));
+      room_accept(rk, o, d, G->room_box[0], G->room_box[1], G->room_box[2], G->room_box[3],
+                  G->room_box[4], G->room_box[5], tmin);
+    }
+    test_group<TP::NTXY>(tests, ntxy, rz, tmin);
+    test_group<TP::NTXZ>(tests + ntxy, ntxz, ry, tmin);
+    test_group<TP::NTYZ>(tests + ntxy + ntxz, ntyz, rx, tmin);
   }
   (void)rect;
   if constexpr (TP::SPH) {
@@ -501,30 +528,39 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     // 32 SGPRs of 8 spheres pushed the SGPR-capped sphere kernel to 65 VGPRs (7 waves/SIMD);
     // at 4 it has 63 (8 waves): C5 at 256 spp 475 -> 467 ms
 #pragma unroll SPT_SPH_UNROLL
-    for (int j = 0; j < nnar; ++j) {
-      const uint32_t kk = tkey(sphere_t(sphs[j], o, d));
-      const bool acc = kk < tmin_key;
-      tmin_key = acc ? kk : tmin_key;
-      pos = acc ? base + j : pos;
-    }
+    for (int j = 0; j < nnar; ++j) tmin = umin(tmin, key_s(sphere_t(sphs[j], o, d), (uint32_t)(base + j)));
     if constexpr (TP::WIDE) {
-      for (int j = nnar; j < nsph; ++j) {  // wide spheres (fp64)
-        const uint32_t kk = tkey(sphere_t_wide(G->sphd[j], o, d));
-        const bool acc = kk < tmin_key;
-        tmin_key = acc ? kk : tmin_key;
-        pos = acc ? base + j : pos;
-      }
+      for (int j = nnar; j < nsph; ++j)  // wide spheres (fp64)
+        tmin = umin(tmin, key_s(sphere_t_wide(G->sphd[j], o, d), (uint32_t)(base + j)));
     }
   }
-  const float tmin = __uint_as_float(tmin_key + 1u);
-  t_out = tmin;
-  // 1/d of the hit rectangle's plane axis (for the hit point's division, see the shading)
+  const bool hit = tmin < kKeyNone;
+  const int pos = (int)(tmin & 63u);  // (63 on a miss: a valid LDS index, the id is kept)
+  // 1/d of the hit rectangle's plane axis (the winner's t and its hit point, see the shading)
   const int nxy = TP::CONSTGEO ? kCornellNXY : n_of<TP>(TP::NXY, G->n_xy);
   const int nxz = TP::CONSTGEO ? kCornellNXZ : n_of<TP>(TP::NXZ, G->n_xz);
   ia_hit = pos < nxy ? iz : (pos < nxy + nxz ? iy : ix);
-  const int idn = keep(pos2idx[pos < 0 ? 0 : pos]);  // (unconditional LDS read: no branch)
-  id = pos >= 0 ? idn : id;
-  return tmin < 1e20f;
+  const int idn = keep(pos2idx[pos]);  // (unconditional LDS read: no branch)
+  id = hit ? idn : id;
+  pos_out = pos;
+  return hit;
+}
+
+// The winner's exact t (contract v5: the t its key was made from), for a hit on prims[id] = H at
+// grouped position pos: a rectangle's (k - o_a) * inv_a, a sphere's nearest root (sphere_t on the
+// same fp32 values as the trace's GeoSph: DevPrim w1..w4 = px, py, pz, r^2), a wide sphere's fp64
+// root.
+template <class TP>
+__device__ __forceinline__ float hit_t(const DevPrim& H, int pos, f3 o, f3 d, float ia,
+                                       const SPT_CONST SceneGeo* G) {
+  if (H.kind == SPT_RECT_XY) return (H.w1 - o.z) * ia;
+  if (H.kind == SPT_RECT_XZ) return (H.w1 - o.y) * ia;
+  if (H.kind == SPT_RECT_YZ) return (H.w1 - o.x) * ia;
+  if constexpr (TP::WIDE) {
+    const int j = pos - (G->n_xy + G->n_xz + G->n_yz);
+    if (j >= G->n_sph - G->n_sph_wide) return sphere_t_wide(G->sphd[j], o, d);
+  }
+  return sphere_t(GeoSph{H.w1, H.w2, H.w3, H.w4, 0, 0, 0, 0}, o, d);
 }
 
 // NEE pre-test (light_sampling :363-369 + the shadow ray of :466): is the light itself accepted
@@ -538,25 +574,26 @@ __device__ __forceinline__ bool light_accepts(const SPT_CONST KParams* P, const 
     static_assert(TP::NXY >= 0 && TP::NXZ >= 0, "LPOS needs static group sizes");
     if constexpr (L < TP::NXY) {
       const RectHit h = rect_eval(rect + L, Ray6{o.z, rcp_nr(d.z), d.x, o.x, d.y, o.y});
-      return h.inb & (tkey(h.tt) < tkey(1e20f));
+      return h.inb & key_valid(h.tt, L);
     } else if constexpr (L < TP::NXY + TP::NXZ) {
       const RectHit h = rect_eval(rect + L, Ray6{o.y, rcp_nr(d.y), d.x, o.x, d.z, o.z});
-      return h.inb & (tkey(h.tt) < tkey(1e20f));
+      return h.inb & key_valid(h.tt, L);
     } else {
       const RectHit h = rect_eval(rect + L, Ray6{o.x, rcp_nr(d.x), d.y, o.y, d.z, o.z});
-      return h.inb & (tkey(h.tt) < tkey(1e20f));
+      return h.inb & key_valid(h.tt, L);
     }
   } else {
     const int lk = P->light_kind, L = P->light_pos;
     if (L < 0) return false;
-    if (lk == SPT_SPHERE)
-      return tkey(TP::WIDE ? sphere_t_any(G, L, o, d) : sphere_t(G->sph[L], o, d)) < tkey(1e20f);
+    const int nrect = G->n_xy + G->n_xz + G->n_yz;
+    if (lk == SPT_SPHERE)  // (light_pos: the index in sph[]; its grouped position follows the rects)
+      return key_valid(TP::WIDE ? sphere_t_any(G, L, o, d) : sphere_t(G->sph[L], o, d), (uint32_t)(nrect + L));
     Ray6 r;
     if (lk == SPT_RECT_XY) r = Ray6{o.z, rcp_nr(d.z), d.x, o.x, d.y, o.y};
     else if (lk == SPT_RECT_XZ) r = Ray6{o.y, rcp_nr(d.y), d.x, o.x, d.z, o.z};
     else r = Ray6{o.x, rcp_nr(d.x), d.y, o.y, d.z, o.z};
     const RectHit h = rect_eval(rect + L, r);
-    return h.inb & (tkey(h.tt) < tkey(1e20f));
+    return h.inb & key_valid(h.tt, (uint32_t)L);
   }
 }
 
@@ -634,12 +671,16 @@ __device__ __forceinline__ float nee_weight(bool unit, f3 d, f3 nl, float t, flo
 }
 constexpr float kRefNeeC = (float)(1296.0 / 3.14159265358979323846);  // kRefLarea / pi
 
-// The jittered raster coordinate (x - 0.5) + u * 2^-16 of :533 (u the 16-bit jitter draw) with
-// f128 = (x - 0.5) - 128: the float with bits 0x4B000000 | u is 2^23 + u exactly, and
-// fma(2^23 + u, 2^-16, f128) rounds the exact sum (x - 0.5) + u * 2^-16 once -- the same bits as
-// fmaf((float)u, 0x1p-16f, x - 0.5f), with a full-rate v_or instead of a half-rate conversion.
-__device__ __forceinline__ float jitter_fma(uint32_t lo, uint32_t hi, float f128) {
-  return fmaf(__uint_as_float(u16i(lo, hi) | 0x4B000000u), 0x1p-16f, f128);
+// The camera ray of contract v5 (oracle c_path, :533-536): per component c
+//   v_c = fma(Fv, Cv_c, fma(Fu, Cu_c, P_c)),  Fu = 2^23 + ju, Fv = 2^23 + jv,
+// with ju, jv the 16-bit jitter draws (the float with bits 0x4B000000 | j is 2^23 + j exactly),
+// Cu_c = hor_c (1/w) 2^-16, Cv_c = ver_c (1/h) 2^-16 per launch and the per-pixel
+// P_c = fma(Au_c, fx, fma(Av_c, fy, llc_c - origin_c)), Au_c = hor_c (1/w), Av_c = ver_c (1/h),
+// fx = (x - 0.5) - 128, fy = (h - y - 1 - 0.5) - 128 (the -128 cancels 2^23 2^-16 in Fu Cu).
+// The axis-aligned camera kernels keep P_x, P_y per work unit: one fma per component per ray
+// (rounds 1-4: the jitter sum, a scale, an fma and a subtract per component).
+__device__ __forceinline__ float jitter_f(uint32_t lo, uint32_t hi) {
+  return __uint_as_float(u16i(lo, hi) | 0x4B000000u);
 }
 
 __device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh) {
@@ -717,7 +758,7 @@ render_kernel(const KParams* __restrict__ Pg) {
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
       s_prims[i] = P->prims[i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
-      if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz) {
+      if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz + 3 * G->has_room) {
         const SPT_CONST GeoTest& q = G->test[i];
         s_test[i] = GeoTest{q.k0, q.k1, q.ma, q.ha, q.mb, q.hb, q.pos0, q.pos1};
       }
@@ -738,7 +779,9 @@ render_kernel(const KParams* __restrict__ Pg) {
   uint32_t lp = 0, s = 0, s_end = 0;
   PxKey pk = PxKey{0, 0, 0};  // Philox round-1/2 terms of the unit's pixel (philox_pixel_key)
   int depth = 0, vid = 0;  // depth: vertices of the current path so far (0 until its first)
-  float fx = 0.0f, fy = 0.0f;  // camera raster terms (x - 0.5) - 128, (h - y - 1 - 0.5) - 128
+  // camera raster terms of the unit's pixel, fx = (x - 0.5) - 128, fy = (h - y - 1 - 0.5) - 128;
+  // the axis-aligned camera kernels hold P_x, P_y (jitter_f) here instead
+  float fx = 0.0f, fy = 0.0f;
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
   // o starts at the camera (the first ray of every sample is a camera ray; the path end resets it)
   f3 o = mk(cptr(Pg)->cam[0], cptr(Pg)->cam[1], cptr(Pg)->cam[2]);
@@ -747,12 +790,12 @@ render_kernel(const KParams* __restrict__ Pg) {
   // ---- wave-uniform state
   // Camera and fixed-point constants of the axis-aligned camera kernels, loaded once and held in
   // SGPRs (each scalar reload in the loop is a wait for the wave).
-  struct CamK { float o0, o1, o2, l0, l1, l2, h0, v1, iw, ih, fs; };
+  struct CamK { float o0, o1, o2, aux, avy, cux, cvy, lx, ly, lz, fs; };
   CamK ck{};
   if constexpr (CF::CAMAX == 1) {
     const SPT_CONST KParams* C = cptr(Pg);
-    ck = CamK{C->cam[0], C->cam[1], C->cam[2], C->cam[3], C->cam[4], C->cam[5], C->cam[6],
-              C->cam[10], C->inv_w, C->inv_h, C->fix_scale};
+    ck = CamK{C->cam[0], C->cam[1], C->cam[2], C->cam_au[0], C->cam_av[1], C->cam_cu[0],
+              C->cam_cv[1], C->cam_l[0], C->cam_l[1], C->cam_l[2], C->fix_scale};
   }
   uint32_t pool_next = 0, pool_end = 0, grab_at = 0;  // grab_at: the wave's last queue position
   bool exhausted = false, capped = false;
@@ -837,6 +880,10 @@ render_kernel(const KParams* __restrict__ Pg) {
         s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
         (void)w;
         pixel_terms(Q, lp, pk, fx, fy);
+        if constexpr (CF::CAMAX == 1) {  // the per-pixel P_x, P_y of the camera ray (jitter_f)
+          fx = fmaf(ck.aux, fx, ck.lx);
+          fy = fmaf(ck.avy, fy, ck.ly);
+        }
 #if SPT_UNIT_SLOTS
         lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
 #endif
@@ -912,16 +959,19 @@ render_kernel(const KParams* __restrict__ Pg) {
       {
         const SPT_CONST KParams* C = cptr(Pg);
         f3 vc;
-        if constexpr (CF::CAMAX == 1) {  // fma(+-0, s, a) == a for a != 0; a == +-0 only meets - o
-          const float su = jitter_fma(r.x, r.y, fx) * ck.iw;
-          const float sv = jitter_fma(r.z, r.w, fy) * ck.ih;
-          vc = mk(fmaf(ck.h0, su, ck.l0) - ck.o0, fmaf(ck.v1, sv, ck.l1) - ck.o1, ck.l2 - ck.o2);
+        const float Fu = jitter_f(r.x, r.y), Fv = jitter_f(r.z, r.w);
+        if constexpr (CF::CAMAX == 1) {
+          // the zero terms vanish exactly: fma(F, +-0, y) == y and fma(+-0, f, L) == L for the
+          // nonzero y, L the host checks (cam_axis)
+          vc = mk(fmaf(Fu, ck.cux, fx), fmaf(Fv, ck.cvy, fy), ck.lz);
         } else {
-          const float su = jitter_fma(r.x, r.y, fx) * C->inv_w;
-          const float sv = jitter_fma(r.z, r.w, fy) * C->inv_h;
-          vc = mk(fmaf(C->cam[9], sv, fmaf(C->cam[6], su, C->cam[3])) - C->cam[0],
-                  fmaf(C->cam[10], sv, fmaf(C->cam[7], su, C->cam[4])) - C->cam[1],
-                  fmaf(C->cam[11], sv, fmaf(C->cam[8], su, C->cam[5])) - C->cam[2]);
+          float vv[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const float Pc = fmaf(C->cam_au[c], fx, fmaf(C->cam_av[c], fy, C->cam_l[c]));
+            vv[c] = fmaf(Fv, C->cam_cv[c], fmaf(Fu, C->cam_cu[c], Pc));
+          }
+          vc = mk(vv[0], vv[1], vv[2]);
         }
         v = mk(cam ? vc.x : v.x, cam ? vc.y : v.y, cam ? vc.z : v.z);  // o: set at the path end
       }
@@ -950,8 +1000,10 @@ render_kernel(const KParams* __restrict__ Pg) {
 #endif
       const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
       int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
-      float t, ia_hit;
-      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), G->sph, s_pos2idx, o, d, t, id, ia_hit);
+      float t = 0.0f, ia_hit;
+      int hpos;
+      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), G->sph, s_pos2idx, o,
+                                     d, id, ia_hit, hpos);
 
       // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467). Then
       //    the light is the next vertex (shaded in the common block below, T = T*f*weight); else the
@@ -968,6 +1020,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         if constexpr (!TP::SPH) ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
         const float nee_c = CF::LREF == 1 ? kRefNeeC : D->nee_c;
+        t = hit_t<TP>(s_prims[id], hpos, o, d, ia_hit, G);  // the light's t (the winner's)
         const float w = lh ? nee_weight(unit_dirs_of<TP>(Pg), d, nl, t, larea, nee_c) : 1.0f;
         T = mk(T.x * w, T.y * w, T.z * w);  // T holds T*f of the shading vertex
         // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
@@ -991,7 +1044,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           const bool kxy = kind == SPT_RECT_XY, kxz = kind == SPT_RECT_XZ, kyz = !kxy && !kxz;
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
-          const float tr = hit_plane_t(H.w1 - oa, da, ia_hit, t);
+          const float n_ = H.w1 - oa;
+          const float tr = hit_plane_t(n_, da, ia_hit, n_ * ia_hit);  // the winner's t, corrected
           x = mk(keep(o.x + d.x * tr), keep(o.y + d.y * tr), keep(o.z + d.z * tr));
           x = hit ? x : mk(0, 0, 0);  // a miss vertex is the origin (:373-374)
           l_miss += hit ? 0u : 1u;
@@ -1003,10 +1057,11 @@ render_kernel(const KParams* __restrict__ Pg) {
           x = mk(0, 0, 0);
           ++l_miss;
         } else {
-          float tr = t;  // plane distance as the reference derives it (:103), see DESIGN.md
-          if (kind == SPT_RECT_XY) tr = hit_plane_t(H.w1 - o.z, d.z, ia_hit, t);
-          else if (kind == SPT_RECT_XZ) tr = hit_plane_t(H.w1 - o.y, d.y, ia_hit, t);
-          else if (kind == SPT_RECT_YZ) tr = hit_plane_t(H.w1 - o.x, d.x, ia_hit, t);
+          // plane distance as the reference derives it (:103); spheres: the root
+          float tr = hit_t<TP>(H, hpos, o, d, ia_hit, G);
+          if (kind == SPT_RECT_XY) tr = hit_plane_t(H.w1 - o.z, d.z, ia_hit, tr);
+          else if (kind == SPT_RECT_XZ) tr = hit_plane_t(H.w1 - o.y, d.y, ia_hit, tr);
+          else if (kind == SPT_RECT_YZ) tr = hit_plane_t(H.w1 - o.x, d.x, ia_hit, tr);
           x = mk(o.x + d.x * tr, o.y + d.y * tr, o.z + d.z * tr);
         }
         // Hitable::normal, oriented against the ray (:123,:166,:209,:251); gn = the unoriented
@@ -1125,14 +1180,18 @@ render_kernel(const KParams* __restrict__ Pg) {
               const uint32_t ldzi = CF::LREF == 1 ? kRefLdzi : D->ldzi;
               const float lx0 = CF::LREF == 1 ? kRefLx0 : D->lx0, lz0 = CF::LREF == 1 ? kRefLz0 : D->lz0;
               if constexpr (CF::LREF == 1) {
-                // ((r >> 8) << 7) * 36 mod 2^32 as one full-rate 24-bit multiply (the operands are
-                // 24 and 13 bits; v_mul_u32_u24 keeps the low 32 bits of the product): the same
-                // bits as the half-rate v_mul_lo_u32 and its mask
-                xl = fmaf((float)(int32_t)__umul24(r.x >> 8, kRefLdxi << 7), 0x1p-31f, lx0);
-                zl = fmaf((float)(int32_t)__umul24(r.y >> 8, kRefLdzi << 7), 0x1p-31f, lz0);
+                // dx = dz = 36 = 4 * 9: the lattice x0 - 1 + m 2^-22, m = r >> 9 (oracle
+                // c_wrap_sample) as fma(2^23 + m, 2^-22, x0 - 3) -- the float with bits
+                // 0x4B000000 | m is 2^23 + m, so the sum is the same real, rounded once: one or and
+                // one fma (rounds 1-4: shift, 24-bit multiply, conversion, fma)
+                static_assert(kRefLdxi == 36u && kRefLdzi == 36u, "LREF light lattice");
+                xl = fmaf(__uint_as_float(0x4B000000u | (r.x >> 9)), 0x1p-22f, lx0 - 3.0f);
+                zl = fmaf(__uint_as_float(0x4B000000u | (r.y >> 9)), 0x1p-22f, lz0 - 3.0f);
               } else {
-                xl = fmaf((float)(int32_t)(((r.x >> 8) << 7) * ldxi), 0x1p-31f, lx0);
-                zl = fmaf((float)(int32_t)(((r.y >> 8) << 7) * ldzi), 0x1p-31f, lz0);
+                xl = D->lx_lattice ? fmaf((float)(r.x >> D->lx_shift), D->lx_scale, D->lx0m1)
+                                   : fmaf((float)(int32_t)(((r.x >> 8) << 7) * ldxi), 0x1p-31f, lx0);
+                zl = D->lz_lattice ? fmaf((float)(r.y >> D->lz_shift), D->lz_scale, D->lz0m1)
+                                   : fmaf((float)(int32_t)(((r.y >> 8) << 7) * ldzi), 0x1p-31f, lz0);
               }
             } else {
               xl = fmaf(u01(r.x), D->ldx, D->lx0);
@@ -1149,13 +1208,13 @@ render_kernel(const KParams* __restrict__ Pg) {
             if constexpr (kEarlyNee) {  // the light's own test (light_accepts), keeping t and a
               const RectHit h = rect_eval(CornellRectPtr{kCornellLightPos},
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
-              la = h.inb & (tkey(h.tt) < tkey(1e20f));
+              la = h.inb & key_valid(h.tt, kCornellLightPos);
               early = la & early_nee_proven(x, h.a);
               t = early ? h.tt : t;  // the t the trace would return (the light's test, same bits)
             } else if constexpr (kEarlySph) {  // the uploaded light rect (XZ, host-checked)
               const RectHit h = rect_eval(G2->rect + D->light_pos,
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
-              la = h.inb & (tkey(h.tt) < tkey(1e20f));
+              la = h.inb & key_valid(h.tt, (uint32_t)D->light_pos);
               early = la & early_room_proven(x, D->early_y0);
               t = early ? h.tt : t;
             } else {
@@ -1186,8 +1245,14 @@ render_kernel(const KParams* __restrict__ Pg) {
             l_early += ea ? 1u : 0u;
             ++l_shadow;
           }
+          // the light's t: the pre-test's for a proven lane, else the traced light hit's own
+          // (k_L - o.y) / d.y as the trace ranked it (the light is an XZ rect in both kernels)
+          float kl;
+          if constexpr (kEarlyNee) kl = kCornellRects[kCornellLightPos].k;
+          else kl = s_prims[kRefLightId].w1;
+          const float tl = ea ? t : (kl - o.y) * ia_hit;
           // (computed for every resolving lane: a branch around it cost exec-mask SALU)
-          const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, t, kRefLarea, kRefNeeC));
+          const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
           const float w = lh ? wl : 1.0f;
           T = mk(T.x * w, T.y * w, T.z * w);
           const DevPrim& H = s_prims[kRefLightId];
@@ -1553,6 +1618,53 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
       }
     }
   }
+  // Contract v5's room (oracle c_find_room): the first XY, XZ, YZ pair tests (test order) whose
+  // planes are exactly -- in the caller's doubles -- the other pairs' in-plane bounds (each pair's
+  // bounds read from its k0 member). Its tests move behind the per-kind lists (the nearest hit is a
+  // minimum of keys, so test order cannot matter).
+  {
+    const int nt = g->n_txy + g->n_txz + g->n_tyz;
+    auto member = [&](int pos) -> const spt_prim& { return s[g->rect[pos].idx]; };
+    auto same_range = [](double k1, double k2, double b1, double b2) {
+      return std::min(k1, k2) == b1 && std::max(k1, k2) == b2;
+    };
+    int room[3] = {-1, -1, -1};
+    for (int a = 0; a < g->n_txy && room[0] < 0; ++a) {
+      const GeoTest& A = g->test[a];
+      if (A.pos0 == A.pos1) continue;
+      for (int b = g->n_txy; b < g->n_txy + g->n_txz && room[0] < 0; ++b) {
+        const GeoTest& B = g->test[b];
+        if (B.pos0 == B.pos1) continue;
+        for (int c = g->n_txy + g->n_txz; c < nt; ++c) {
+          const GeoTest& D = g->test[c];
+          if (D.pos0 == D.pos1) continue;
+          const double* ga = member(A.pos0).geom, *gb = member(B.pos0).geom, *gd = member(D.pos0).geom;
+          const double zA = ga[4], zB = member(A.pos1).geom[4], yA = gb[4], yB = member(B.pos1).geom[4];
+          const double xA = gd[4], xB = member(D.pos1).geom[4];
+          if (!same_range(xA, xB, ga[0], ga[1]) || !same_range(xA, xB, gb[0], gb[1]) ||
+              !same_range(yA, yB, ga[2], ga[3]) || !same_range(yA, yB, gd[0], gd[1]) ||
+              !same_range(zA, zB, gb[2], gb[3]) || !same_range(zA, zB, gd[2], gd[3]))
+            continue;
+          room[0] = a; room[1] = b; room[2] = c;
+          break;
+        }
+      }
+    }
+    g->has_room = room[0] >= 0;
+    if (g->has_room) {
+      const GeoTest A = g->test[room[0]], B = g->test[room[1]], D = g->test[room[2]];
+      g->room_box[0] = A.ma; g->room_box[1] = A.ha + 0x1p-8f;
+      g->room_box[2] = A.mb; g->room_box[3] = A.hb + 0x1p-8f;
+      g->room_box[4] = B.mb; g->room_box[5] = B.hb + 0x1p-8f;
+      GeoTest rest[kMaxPrims];
+      int n = 0;
+      for (int i = 0; i < nt; ++i)
+        if (i != room[0] && i != room[1] && i != room[2]) rest[n++] = g->test[i];
+      for (int i = 0; i < n; ++i) g->test[i] = rest[i];
+      g->test[n] = A; g->test[n + 1] = B; g->test[n + 2] = D;
+      --g->n_txy; --g->n_txz; --g->n_tyz;
+    }
+  }
   // Spheres in index order, the narrow (fp32) ones first, then the wide (fp64) ones (oracle
   // c_intersect): the kernel's fp32 loop carries no per-sphere precision test.
   for (int pass = 0; pass < 2; ++pass)
@@ -1587,8 +1699,16 @@ static void magic31(uint32_t d, uint32_t* m, uint32_t* sh) {
 // Does the uploaded scene's grouped geometry equal the compile-time HEAD scene bit for bit?
 static bool cornell_const_match(const SceneGeo& g, int light_pos) {
   if (g.n_xy != kCornellNXY || g.n_xz != kCornellNXZ || g.n_yz != kCornellNYZ || g.n_sph != 0 ||
-      light_pos != kCornellLightPos)
+      light_pos != kCornellLightPos || !g.has_room)
     return false;
+  {  // the same room (tests behind the per-kind lists) and box as the compile-time kCornellRoom
+    const int nt = g.n_txy + g.n_txz + g.n_tyz;
+    for (int r = 0; r < 3; ++r) {
+      const CTest& C = kCornellTests.t[kCornellRoom[r]];
+      if (g.test[nt + r].pos0 != C.pos0 || g.test[nt + r].pos1 != C.pos1) return false;
+    }
+    if (std::memcmp(g.room_box, kCornellRoomDef.box, sizeof g.room_box) != 0) return false;
+  }
   for (int i = 0; i < kCornellNXY + kCornellNXZ + kCornellNYZ; ++i) {
     const GeoRect& R = g.rect[i];
     const CRect& C = kCornellRects[i];
@@ -1745,12 +1865,16 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                                                         : 3;
   const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
                        g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8 &&
-                       g.n_txy == 3 && g.n_txz == 4 && g.n_tyz == 3;
+                       g.n_txy == 2 && g.n_txz == 3 && g.n_tyz == 2 && g.has_room;
   const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
   // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
   // axis-aligned camera (Cfg CAMAX): horizontal.y/z and vertical.x/z zero, origin nonzero
-  bool cam_axis = K.cam[7] == 0.0f && K.cam[8] == 0.0f && K.cam[9] == 0.0f && K.cam[11] == 0.0f &&
-                  K.cam[0] != 0.0f && K.cam[1] != 0.0f && K.cam[2] != 0.0f;
+  // (the contract-v5 terms L = llc - origin and Au_x, Av_y nonzero: the zero products then vanish
+  // exactly, see the kernel's camera ray)
+  bool cam_axis = K.cam[7] == 0.0f && K.cam[8] == 0.0f && K.cam[9] == 0.0f && K.cam[11] == 0.0f;
+  for (int c = 0; c < 3; ++c) cam_axis = cam_axis && (K.cam[3 + c] - K.cam[c]) != 0.0f;
+  cam_axis = cam_axis && K.cam[6] * (1.0f / (float)p->width) != 0.0f &&
+             K.cam[10] * (1.0f / (float)p->height) != 0.0f;
   for (int i = 0; i < 12; ++i) cam_axis = cam_axis && std::isfinite(K.cam[i]);
   const bool lref = p->rr_depth == kRefRrDepth && p->light_id == kRefLightId &&
                     p->light_x0 == kRefLx0 && p->light_dx == 36.0f && p->light_z0 == kRefLz0 &&
@@ -1850,6 +1974,25 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.fix_scale = K.inv_spp * 2147483648.0f;
   K.inv_w = 1.0f / (float)p->width;
   K.inv_h = 1.0f / (float)p->height;
+  for (int c = 0; c < 3; ++c) {  // camera of contract v5 (oracle c_path)
+    K.cam_au[c] = K.cam[6 + c] * K.inv_w;
+    K.cam_av[c] = K.cam[9 + c] * K.inv_h;
+    K.cam_cu[c] = K.cam_au[c] * 0x1p-16f;
+    K.cam_cv[c] = K.cam_av[c] * 0x1p-16f;
+    K.cam_l[c] = K.cam[3 + c] - K.cam[c];
+  }
+  {  // light sample lattice of contract v5 (oracle c_wrap_sample)
+    auto lattice = [](uint32_t dx, float x0, int* on, uint32_t* shift, float* scale, float* x0m1) {
+      int a = 0;
+      while (a < 32 && dx != 0 && !((dx >> a) & 1u)) ++a;
+      *on = dx != 0 && a >= 1 && a <= 24;
+      *shift = *on ? 7u + (uint32_t)a : 0u;
+      *scale = std::ldexp(1.0f, a - 24);
+      *x0m1 = x0 - 1.0f;
+    };
+    lattice(K.ldxi, K.lx0, &K.lx_lattice, &K.lx_shift, &K.lx_scale, &K.lx0m1);
+    lattice(K.ldzi, K.lz0, &K.lz_lattice, &K.lz_shift, &K.lz_scale, &K.lz0m1);
+  }
   K.accum = c->accum;
 #if SPT_UNIT_SLOTS
   if (3ull * n_units > c->slots_cap) {  // one owner store per unit (24 B): C3 208 MB, C4/C5 ~400 MB

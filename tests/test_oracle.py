@@ -217,10 +217,13 @@ def test_counter_mode_pins(oracle):
 
 @pytest.mark.parametrize("est,q", [("nee", 1.0), ("cos", 0.0)])
 def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
-    """The contract's parallel-pair rect tests (one plane of a box's opposite faces per ray) give
-    the same image and path statistics as testing every rectangle on its own (intersect
-    :323-335 as written): the skipped plane is never the nearest hit outside ulp-level edge
-    grazes, which do not occur in 1.6 M samples (measured: 0 differing pixels in 3.1 M)."""
+    """The contract's parallel-pair rect tests (one plane of a box's opposite faces per ray) and its
+    room test (the nearest of the three wall pairs, one box check widened by 2^-8: contract v5)
+    against testing every rectangle on its own (intersect :323-335 as written). The skipped plane of
+    a pair is never the nearest hit outside ulp-level edge grazes; the room rule differs only for
+    rays from outside the room (leaked paths) that pass within 2^-8 of a wall's edge. Measured at
+    128x96, seed 7: misses 348289 vs 348488 (-0.06 %), 4 of 12288 pixels differ by <= 2.7e-4 (NEE);
+    cosine-only: 0 pixels (the leaked paths carry no light)."""
     prims = oracle.scene_cornell()
     p = oracle.default_params(width=128, height=96, spp=128 if est == "nee" else 64, seed=7,
                               nee_prob=q)
@@ -230,7 +233,12 @@ def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
         b, sb = oracle.counter_render(prims, oracle.camera(128 / 96), p)
     finally:
         oracle.set_pairs(True)
-    assert np.array_equal(a, b) and sa == sb
+    d = np.abs(a.astype(np.float64) - b)
+    assert (d.max(axis=2) > 0).sum() <= 0.001 * d.shape[0] * d.shape[1] and d.max() < 1e-3
+    assert sa["samples"] == sb["samples"]
+    for k in ("path_rays", "vertices", "nee_light_hits", "cosine_samples", "shadow_traced"):
+        assert abs(sa[k] - sb[k]) <= 1e-5 * sa["samples"] * 10, (k, sa[k], sb[k])
+    assert abs(sa["misses"] / sb["misses"] - 1) < 2e-3, (sa["misses"], sb["misses"])
 
 
 @pytest.mark.parametrize("pairs", [True, False])
