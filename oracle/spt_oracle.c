@@ -767,8 +767,14 @@ static void c_find_room(c_ctx* C, const spt_prim* s) {
  * the lower position (the reference: strict `<` over rect[] :328, ties to the lower index). On the
  * GPU a key is one v_add and one v_bitop3, and the running minimum one v_min_u32 -- no compare and
  * lane-mask select per candidate. */
-static inline uint32_t c_key(float t, int pos) { return ((asu(t) - 1u) | 63u) ^ (uint32_t)(63 - pos); }
-#define C_KEY_NONE ((asu(1e20f) - 1u) | 63u) /* tmin = 1e20 (:324): no hit */
+static inline uint32_t c_key(float t, int pos) { return (asu(t) | 63u) ^ (uint32_t)(63 - pos); }
+#define C_KEY_NONE (asu(1e20f) | 63u) /* tmin = 1e20 (:324): no hit */
+/* A plane's distance in contract v5: t = (k - o_a) * inv_a as one fma with -2^-149 added. That is
+ * the rounded product except when the product is an exact rounding tie (then the lower neighbour)
+ * and turns a zero distance (the origin on the plane: :106 `t<0`, :328 `d != 0` reject it) into
+ * -2^-149, which ranks last like every negative t: the key needs no "minus one" to put +0 last. */
+#define C_NEG_TINY (-0x1p-149f)
+static inline float c_plane_t(float n, float inv) { return fmaf(n, inv, C_NEG_TINY); }
 static inline uint32_t c_umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 /* The counter-mode scene intersection (intersect :323-335). inv = rcp_nr(d) once per ray.
@@ -796,11 +802,11 @@ static float c_sphere_wide(const c_prim* P, fv o, fv d) {
   const double qx = fma(-k, dx, ox), qy = fma(-k, dy, oy), qz = fma(-k, dz, oz);
   const double det = P->drad2 - fma(qz, qz, fma(qy, qy, qx * qx));
   double sd, t1, t2;
-  if (!(det >= 0.0)) return 0.0f;
+  if (!(det >= 0.0)) return -0.0f;
   sd = sqrt(det / a);
   t1 = k - sd;
   t2 = k + sd;
-  return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
+  return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : -0.0)); /* -0: no root (ranks last) */
 }
 
 /* A narrow sphere in fp32: det = b^2 - op.op + r^2 (:233, as one fma), the nearest root beyond
@@ -814,11 +820,11 @@ static float c_sphere(const c_prim* P, fv o, fv d) {
   const float bb = fdot(op, d);
   const float det = fmaf(bb, bb, P->rad2 - fdot(op, op)); /* :233's b*b - op.op + rad*rad */
   float sd, t1, t2;
-  if (!(det >= 0.0f)) return 0.0f;
+  if (!(det >= 0.0f)) return -0.0f;
   sd = det * spt_oracle_rsq_nr2(det); /* two Newton steps (round 3): 5e-6 relative */
   t1 = bb - sd;
   t2 = bb + sd;
-  return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+  return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : -0.0f); /* -0: no root (ranks last) */
 }
 
 /* Does the light itself accept the ray (o, d)? Its own test, exactly as inside c_intersect (the
@@ -833,18 +839,17 @@ static int c_light_accepts(const c_ctx* C, fv o, fv d) {
   if (P->kind == SPT_SPHERE)
     return c_key(P->wide ? c_sphere_wide(P, o, d) : c_sphere(P, o, d), C->light_pos) < C_KEY_NONE;
   {
-    float oa, da, tt, tb, a, b;
+    float oa, da, tt, a, b;
     switch (P->kind) {
       case SPT_RECT_XY: oa = o.z; da = d.z; break;
       case SPT_RECT_XZ: oa = o.y; da = d.y; break;
       default: oa = o.x; da = d.x; break;
     }
-    tt = (P->k - oa) * spt_oracle_rcp_nr(da);
-    tb = asf(asu(tt) - 1u); /* the in-plane test at t- (contract v5, c_intersect) */
+    tt = c_plane_t(P->k - oa, spt_oracle_rcp_nr(da)); /* as inside c_intersect (contract v5) */
     switch (P->kind) {
-      case SPT_RECT_XY: a = fmaf(d.x, tb, o.x - P->ma); b = fmaf(d.y, tb, o.y - P->mb); break;
-      case SPT_RECT_XZ: a = fmaf(d.x, tb, o.x - P->ma); b = fmaf(d.z, tb, o.z - P->mb); break;
-      default: a = fmaf(d.y, tb, o.y - P->ma); b = fmaf(d.z, tb, o.z - P->mb); break;
+      case SPT_RECT_XY: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.y, tt, o.y - P->mb); break;
+      case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
+      default: a = fmaf(d.y, tt, o.y - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
     }
     return fabsf(a) <= P->ha && fabsf(b) <= P->hb && c_key(tt, C->light_pos) < C_KEY_NONE;
   }
@@ -859,8 +864,8 @@ static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0
 static float g_proof_y0;
 static uint64_t g_proof_n, g_proof_bad;
 static int c_early_nee_proven(fv o, fv d, float* tl) {
-  const float tt = (81.5f - o.y) * spt_oracle_rcp_nr(d.y), tb = asf(asu(tt) - 1u);
-  const float a = fmaf(d.x, tb, o.x - 50.0f), b = fmaf(d.z, tb, o.z - 79.5f);
+  const float tt = c_plane_t(81.5f - o.y, spt_oracle_rcp_nr(d.y));
+  const float a = fmaf(d.x, tt, o.x - 50.0f), b = fmaf(d.z, tt, o.z - 79.5f);
   const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && c_key(tt, 8) < C_KEY_NONE;
   const int room = asu(o.x) - asu(1.0f) <= asu(99.0f) - asu(1.0f) && asu(o.z) <= asu(170.0f) &&
                    asu(o.y) < asu(81.5f);
@@ -885,9 +890,9 @@ void spt_oracle_proof_counts(uint64_t out[2]) {
  *  - a rect test gives one key per plane, t = (k - o_a) * inv_a; a parallel PAIR's candidate is
  *    the smaller of its two planes' keys -- the smaller positive t, which is exactly the plane the
  *    rounds-1-4 pair rule chose (the one ahead and nearer; the planes of a pair are >= 25 units
- *    apart, far more than the keys' 64 ulps) -- and its in-plane test is evaluated at
- *    t- = float(min(bits(t0) - 1, bits(t1) - 1)), the float just below the chosen t; a single's at
- *    float(bits(t) - 1). Accepted iff |a| <= half and |b| <= half there (:104-106);
+ *    apart, far more than the keys' 64 ulps) -- and its in-plane test is evaluated at the chosen
+ *    t (c_plane_t: the distance as one fma with -2^-149). Accepted iff |a| <= half and
+ *    |b| <= half there (:104-106);
  *  - the ROOM (c_find_room) is one box: the smallest of its three pairs' keys is the candidate, and
  *    it is accepted iff its point at t_R = float(key) lies in the room box widened by 2^-8 on every
  *    axis. For an origin in the room the nearest of the three exit planes always lies in the box
@@ -914,14 +919,14 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     }
     if (room) continue; /* below */
     {
-      const float t0 = (T->k0 - oa) * ia;
+      const float t0 = c_plane_t(T->k0 - oa, ia);
       if (T->id0 != T->id1) {
-        const float t1 = (T->k1 - oa) * ia;
+        const float t1 = c_plane_t(T->k1 - oa, ia);
         kp = c_umin(c_key(t0, T->pos0), c_key(t1, T->pos1));
-        tb = asf(c_umin(asu(t0) - 1u, asu(t1) - 1u));
+        tb = asf(c_umin(asu(t0), asu(t1)));
       } else {
         kp = c_key(t0, T->pos0);
-        tb = asf(asu(t0) - 1u);
+        tb = t0;
       }
     }
     /* in-plane offsets from the rectangle's centre, a = d_b * t + (o_b - mid_b) in one fma */
@@ -938,7 +943,7 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     for (r = 0; r < 3; r++) {
       const c_test* T = &C->tests[C->room[r]];
       const float oa = r == 0 ? o.z : (r == 1 ? o.y : o.x), ia = r == 0 ? iz : (r == 1 ? iy : ix);
-      rk = c_umin(rk, c_umin(c_key((T->k0 - oa) * ia, T->pos0), c_key((T->k1 - oa) * ia, T->pos1)));
+      rk = c_umin(rk, c_umin(c_key(c_plane_t(T->k0 - oa, ia), T->pos0), c_key(c_plane_t(T->k1 - oa, ia), T->pos1)));
     }
     {
       const float tr = asf(rk);
@@ -962,9 +967,9 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   {
     const c_prim* H = &C->prims[*id];
     switch (H->kind) {
-      case SPT_RECT_XY: *t = (H->k - o.z) * iz; break;
-      case SPT_RECT_XZ: *t = (H->k - o.y) * iy; break;
-      case SPT_RECT_YZ: *t = (H->k - o.x) * ix; break;
+      case SPT_RECT_XY: *t = c_plane_t(H->k - o.z, iz); break;
+      case SPT_RECT_XZ: *t = c_plane_t(H->k - o.y, iy); break;
+      case SPT_RECT_YZ: *t = c_plane_t(H->k - o.x, ix); break;
       default: *t = H->wide ? c_sphere_wide(H, o, d) : c_sphere(H, o, d);
     }
   }

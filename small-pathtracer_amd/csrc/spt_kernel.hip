@@ -302,32 +302,38 @@ __device__ __forceinline__ Ray6 ray6(f3 o, f3 d, float ix, float iy, float iz) {
 }
 
 // ---- Nearest hit, contract v5 (round 4; oracle c_intersect / c_key). A candidate at t on the plane
-// or sphere with grouped position pos is ranked by its KEY: the bits of t minus one (so 0 < t < tmin
-// stays one unsigned compare; +-0, negatives, inf and NaN rank last) with the low 6 bits replaced
-// by pos; the nearest hit is the smallest key. Per candidate that is one v_add, one v_bitop3 and
-// one v_min_u32 -- where rounds 1-4 compared keys and selected (t, position) through lane masks,
-// a v_cmp -> s_and -> two v_cndmask chain per test: C3 13.56 -> 12.92 ms (A/B, profiles/r04_ab.txt).
+// or sphere with grouped position pos is ranked by its KEY: the float bits of t with the low 6 bits
+// replaced by pos (negatives, inf and NaN rank last; a plane's zero distance is -2^-149, plane_t,
+// and a sphere without a root -0); the nearest hit is the smallest key. Per candidate that is one
+// v_bitop3 and one v_min_u32 -- where rounds 1-4 compared keys and selected (t, position) through
+// lane masks, a v_cmp -> s_and -> two v_cndmask chain per test: C3 13.55 -> 12.75 ms, and the
+// fma'd -2^-149 that spares the key's "minus one" ... (A/B, profiles/r04_ab.txt).
 // A parallel pair's candidate is the smaller of its two planes' keys (the smaller positive t: the
-// plane the rounds-1-4 pair rule chose); its in-plane test is evaluated at t- = the float below the
-// chosen t. The winner's exact t is recomputed by whoever needs it (shading, NEE weight) from its
-// plane or sphere: the same bits as in its key.
-constexpr uint32_t kKeyNone = (__builtin_bit_cast(uint32_t, 1e20f) - 1u) | 63u;  // tmin = 1e20 (:324)
+// plane the rounds-1-4 pair rule chose); its in-plane test is evaluated at that plane's t. The
+// winner's exact t is recomputed by whoever needs it (shading, NEE weight) from its plane or
+// sphere: the same bits as in its key.
+constexpr uint32_t kKeyNone = __builtin_bit_cast(uint32_t, 1e20f) | 63u;  // tmin = 1e20 (:324)
+// A plane's distance (oracle c_plane_t): (k - o_a) * inv_a as one fma with -2^-149 -- the rounded
+// product except at an exact rounding tie, and a zero distance (origin on the plane: :106, :328
+// reject it) becomes -2^-149 and ranks last like every negative t, so the key needs no "minus one".
+constexpr float kNegTiny = -0x1p-149f;
+__device__ __forceinline__ float plane_t(float n, float inv) { return fmaf(n, inv, kNegTiny); }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
-// ((bits(t) - 1) | 63) ^ (63 - pos) as ONE v_bitop3 (0x36 = (S0 | S2) ^ S1) after the v_add
+// (bits(t) | 63) ^ (63 - pos) as ONE v_bitop3 (0x36 = (S0 | S2) ^ S1)
 template <int POS>
 __device__ __forceinline__ uint32_t key_c(float t) {  // compile-time position (inline constant)
   uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t) - 1u), "n"(63 - POS));
+  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t)), "n"(63 - POS));
   return r;
 }
 __device__ __forceinline__ uint32_t key_v(float t, uint32_t pos) {  // position in a VGPR
   uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t) - 1u), "v"(63u - pos));
+  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t)), "v"(63u - pos));
   return r;
 }
 __device__ __forceinline__ uint32_t key_s(float t, uint32_t pos) {  // wave-uniform position (SGPR)
   uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t) - 1u), "s"(63u - pos));
+  asm("v_bitop3_b32 %0, %1, %2, 63 bitop3:0x36" : "=v"(r) : "v"(__float_as_uint(t)), "s"(63u - pos));
   return r;
 }
 
@@ -351,15 +357,15 @@ __device__ __forceinline__ void plane_keys(const SPT_CONST GeoTest* g, float t0,
 }
 template <int J, bool PAIR, class GP>
 __device__ __forceinline__ void rect_cand(GP g, const Ray6& r, uint32_t& tmin) {
-  const float t0 = (g->k0 - r.oa) * r.ia;
+  const float t0 = plane_t(g->k0 - r.oa, r.ia);
   float t1 = t0;
-  uint32_t kb = __float_as_uint(t0) - 1u, kp;
+  uint32_t kb = __float_as_uint(t0), kp;
   if constexpr (PAIR) {
-    t1 = (g->k1 - r.oa) * r.ia;
-    kb = umin(kb, __float_as_uint(t1) - 1u);
+    t1 = plane_t(g->k1 - r.oa, r.ia);
+    kb = umin(kb, __float_as_uint(t1));
   }
   plane_keys<J, PAIR>(g, t0, t1, kp);
-  const float tb = __uint_as_float(kb);  // t- of the chosen plane
+  const float tb = __uint_as_float(kb);  // the chosen plane's t
   // in-plane offsets from the centre, a = d_b * t + (o_b - mid_b): the origin's offset is per ray
   // and shared by every rectangle with that centre (CSE'd across the unrolled tests)
   const float a = fmaf(r.db, tb, r.ob - g->ma), b = fmaf(r.dc, tb, r.oc - g->mb);
@@ -369,7 +375,7 @@ __device__ __forceinline__ void rect_cand(GP g, const Ray6& r, uint32_t& tmin) {
 // The room's pair (oracle c_intersect, the room): the smaller key of its two planes, no bounds.
 template <int J, class GP>
 __device__ __forceinline__ uint32_t room_pair(GP g, const Ray6& r) {
-  const float t0 = (g->k0 - r.oa) * r.ia, t1 = (g->k1 - r.oa) * r.ia;
+  const float t0 = plane_t(g->k0 - r.oa, r.ia), t1 = plane_t(g->k1 - r.oa, r.ia);
   uint32_t kp;
   plane_keys<J, true>(g, t0, t1, kp);
   return kp;
@@ -410,14 +416,16 @@ __device__ __forceinline__ void test_group(GT g, int n_rt, const Ray6& r, uint32
 struct RectHit { float tt; bool inb; float a; };  // a: first in-plane offset from the centre
 template <class GP>
 __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
-  const float tt = (g->k - r.oa) * r.ia, tb = __uint_as_float(__float_as_uint(tt) - 1u);
-  const float a = fmaf(r.db, tb, r.ob - g->ma), b = fmaf(r.dc, tb, r.oc - g->mb);
+  const float tt = plane_t(g->k - r.oa, r.ia);
+  const float a = fmaf(r.db, tt, r.ob - g->ma), b = fmaf(r.dc, tt, r.oc - g->mb);
   const bool ia = fabsf(a) <= g->ha, ib = fabsf(b) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib), a};
 }
-// A candidate at t with position pos can be the nearest hit at all: its key ranks below "none".
+// A candidate at t with position pos can be the nearest hit at all: its key
+// (bits(t) | 63) ^ (63 - pos) ranks below kKeyNone = bits(1e20) | 63, i.e. bits(t) <= kKeyNone for
+// pos < 63 (one compare) and bits(t) < kKeyNone & ~63 for pos 63.
 __device__ __forceinline__ bool key_valid(float t, uint32_t pos) {
-  return (((__float_as_uint(t) - 1u) | 63u) ^ (63u - pos)) < kKeyNone;
+  return pos < 63u ? __float_as_uint(t) <= kKeyNone : __float_as_uint(t) < (kKeyNone & ~63u);
 }
 
 template <class SP>
@@ -428,14 +436,14 @@ __device__ __forceinline__ float sphere_t(const SP& S, f3 o, f3 d) {
   const f3 op = mk(S.px - o.x, S.py - o.y, S.pz - o.z);
   const float bb = dot3(op, d);
   const float det = fmaf(bb, bb, S.rad2 - dot3(op, op));
-  if (!(det >= 0.0f)) return 0.0f;
+  if (!(det >= 0.0f)) return -0.0f;  // no root: -0 ranks last (contract v5 key)
   // the root as det * rsq_nr2(det) (contract, oracle c_sphere): the IEEE sqrtf sequence costs ~18
   // issue slots, det * rsq_nr(det) 13 (round 2: C5 at 256 spp 452.8 -> 427.3 ms), two Newton steps
   // 10 (round 3: the root within 5e-6 relative, 3e-5 at r = 6, far below the 2e-3 epsilon);
   // det = 0 gives 0
   const float sd = det * rsq_nr2(det);
   const float t1 = bb - sd, t2 = bb + sd;
-  return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : 0.0f);
+  return t1 > 2e-3f ? t1 : (t2 > 2e-3f ? t2 : -0.0f);
 }
 
 // A wide sphere (the 1e5 walls and the radius-600 light of the classic smallpt box) in fp64: the
@@ -451,10 +459,10 @@ __device__ __forceinline__ float sphere_t_wide(const SPT_CONST GeoSphD& S, f3 o,
   const double k = fma(oz, dz, fma(oy, dy, ox * dx)) / a;
   const double qx = fma(-k, dx, ox), qy = fma(-k, dy, oy), qz = fma(-k, dz, oz);
   const double det = S.rad2 - fma(qz, qz, fma(qy, qy, qx * qx));
-  if (!(det >= 0.0)) return 0.0f;
+  if (!(det >= 0.0)) return -0.0f;
   const double sd = sqrt(det / a);
   const double t1 = k - sd, t2 = k + sd;
-  return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : 0.0));
+  return (float)(t1 > 2e-3 ? t1 : (t2 > 2e-3 ? t2 : -0.0));
 }
 __device__ __forceinline__ float sphere_t_any(const SPT_CONST SceneGeo* G, int j, f3 o, f3 d) {
   if (G->sph[j].wide) return sphere_t_wide(G->sphd[j], o, d);  // wave-uniform (scalar load)
@@ -553,9 +561,9 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
 template <class TP>
 __device__ __forceinline__ float hit_t(const DevPrim& H, int pos, f3 o, f3 d, float ia,
                                        const SPT_CONST SceneGeo* G) {
-  if (H.kind == SPT_RECT_XY) return (H.w1 - o.z) * ia;
-  if (H.kind == SPT_RECT_XZ) return (H.w1 - o.y) * ia;
-  if (H.kind == SPT_RECT_YZ) return (H.w1 - o.x) * ia;
+  if (H.kind == SPT_RECT_XY) return plane_t(H.w1 - o.z, ia);
+  if (H.kind == SPT_RECT_XZ) return plane_t(H.w1 - o.y, ia);
+  if (H.kind == SPT_RECT_YZ) return plane_t(H.w1 - o.x, ia);
   if constexpr (TP::WIDE) {
     const int j = pos - (G->n_xy + G->n_xz + G->n_yz);
     if (j >= G->n_sph - G->n_sph_wide) return sphere_t_wide(G->sphd[j], o, d);
@@ -1045,7 +1053,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
           const float n_ = H.w1 - oa;
-          const float tr = hit_plane_t(n_, da, ia_hit, n_ * ia_hit);  // the winner's t, corrected
+          const float tr = hit_plane_t(n_, da, ia_hit, plane_t(n_, ia_hit));  // the winner's t, corrected
           x = mk(keep(o.x + d.x * tr), keep(o.y + d.y * tr), keep(o.z + d.z * tr));
           x = hit ? x : mk(0, 0, 0);  // a miss vertex is the origin (:373-374)
           l_miss += hit ? 0u : 1u;
@@ -1250,7 +1258,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           float kl;
           if constexpr (kEarlyNee) kl = kCornellRects[kCornellLightPos].k;
           else kl = s_prims[kRefLightId].w1;
-          const float tl = ea ? t : (kl - o.y) * ia_hit;
+          const float tl = ea ? t : plane_t(kl - o.y, ia_hit);
           // (computed for every resolving lane: a branch around it cost exec-mask SALU)
           const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
           const float w = lh ? wl : 1.0f;
