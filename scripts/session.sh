@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
-# Round-3 measurement session on the GPU box (in-tree build): GPU tests, the C3 rocprofv3 session
-# (kernel trace + separate PMC passes, scripts/profile.sh), instruction-class PMC passes for C3 and
-# C5, and the bench lines of every config (C2-C5, with their CPU baselines).
+# Measurement session on the GPU box (in-tree build): GPU tests, the C3 rocprofv3 session (kernel
+# trace + separate PMC passes, scripts/profile.sh), instruction-class PMC passes, and the bench lines
+# of every config (C2-C5, with their CPU baselines). Outputs are tagged with TAG (default r04).
 #   PARTS="pytest smoke rehearsal profile classes bench" selects parts; each GPU step has its own time limit and the
 #   script stops at the first failure.
 set -u
@@ -9,6 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 PARTS=${PARTS:-"pytest profile classes bench"}
+TAG=${TAG:-r04}
 has() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
 if has pytest; then
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
@@ -23,7 +24,7 @@ if has rehearsal; then  # the N>1 bench path on the one GPU (gloo gather; RCCL n
   RANKS="${RANKS:-2 4}" bash scripts/rehearsal_r02.sh || exit $?
 fi
 if has profile; then
-  bash scripts/profile.sh r03 || exit $?
+  bash scripts/profile.sh $TAG || exit $?
 fi
 if has classes; then
   # CLS: configurations (tag[:chunk]); c2:32 = C2 at 32-sample units (the C2 tail study)
@@ -50,7 +51,7 @@ if has bench; then
   for cfg in c3 c2 c4 c5; do
     st=5; [ $cfg = c4 ] && st=3; [ $cfg = c5 ] && st=2
     timeout -k 10 420 python bench.py --config $cfg --steps $st --warmup 1 \
-      > gpurun_out/r03_bench_$cfg.json 2> gpurun_out/r03_bench_$cfg.err
+      > gpurun_out/${TAG}_bench_$cfg.json 2> gpurun_out/${TAG}_bench_$cfg.err
     rc=$?; echo "bench $cfg exit $rc"; [ $rc -eq 0 ] || exit $rc
   done
 fi

@@ -73,6 +73,13 @@ constexpr CRect kCornellRects[17] = {
     crect(0, 81.6, 0, 170, 1, 2), crect(0, 81.6, 0, 170, 99, 3), crect(0, 50, 32, 62, 12, 9),
     crect(0, 50, 32, 62, 42, 10), crect(0, 25, 63, 88, 63, 14), crect(0, 25, 63, 88, 88, 15)};
 constexpr int kCornellNXY = 6, kCornellNXZ = 5, kCornellNYZ = 6, kCornellLightPos = 8;
+constexpr int cornell_pos_of(int idx) {
+  for (int i = 0; i < 17; ++i)
+    if (kCornellRects[i].idx == idx) return i;
+  return -1;
+}
+constexpr int kCornellPosOfPrim0 = cornell_pos_of(0);  // Front (:288), XY
+static_assert(kCornellPosOfPrim0 == 0, "prim 0 is the first XY rect");
 
 // The contract's rect tests over the grouped list (oracle c_build_tests): inside each kind group,
 // in order, a rectangle pairs with the first later unpaired one of bit-identical bounds on a

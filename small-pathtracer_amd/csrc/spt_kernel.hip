@@ -543,7 +543,10 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     }
   }
   const bool hit = tmin < kKeyNone;
-  const int pos = (int)(tmin & 63u);  // (63 on a miss: a valid LDS index, the id is kept)
+  int pos = (int)(tmin & 63u);  // (63 on a miss: a valid LDS index, the id is kept)
+  // HEAD kernels: a miss reports the position of prim 0, whose id a missed path ray keeps (:373-374),
+  // so the shading takes the hit's plane axis from the same two position compares as ia_hit
+  if constexpr (TP::CONSTGEO) pos = hit ? pos : kCornellPosOfPrim0;
   // 1/d of the hit rectangle's plane axis (the winner's t and its hit point, see the shading)
   const int nxy = TP::CONSTGEO ? kCornellNXY : n_of<TP>(TP::NXY, G->n_xy);
   const int nxz = TP::CONSTGEO ? kCornellNXZ : n_of<TP>(TP::NXZ, G->n_xz);
@@ -846,15 +849,19 @@ render_kernel(const KParams* __restrict__ Pg) {
 #endif
     const SPT_CONST KParams* P = cptr(Pg);
     SPT_REGION(0);  // loop iteration
-    if (iter >= kMaxWaveIters) {  // runaway guard: drop the work, leave through the normal exit
-      capped = true;                // (a second loop exit would duplicate the loop state)
-      exhausted = true;
+    if (__builtin_expect(iter >= kMaxWaveIters, 0)) {  // runaway guard: drop the work, leave
+      capped = true;                // through the normal exit (a second loop exit would duplicate
+      exhausted = true;             // the loop state)
       ls = kStIdle;
     }
     // 1) (a unit is retired at the end of its last sample, in the path-end block below)
     // 2) refill idle lanes from the wave's pool (ballot + mbcnt prefix sum), pool from the queue.
+    //    Everything up to the loop exit test runs only when some lane is idle: most iterations
+    //    skip it with one wave-uniform branch (round 4: the loop-head bookkeeping was ~12 SALU per
+    //    iteration when no lane needed a unit).
+    uint64_t need = __ballot(ls == kStIdle);
+    if (need != 0) {
     bool needs_unit = ls == kStIdle;
-    uint64_t need = __ballot(needs_unit);
     while (need != 0 && !exhausted) {
       SPT_REGION(2);
       const SPT_CONST KParams* Q = cptr(Pg);
@@ -948,6 +955,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       }
     }
     if (__ballot(ls != kStIdle) == 0) break;
+    }
     n_cos += (uint32_t)__popcll(__ballot(ls == kStCos));
 
     // 3) generate the path ray (kStCam, kStCos, kStSpec): the cosine continuation from the last
@@ -1049,7 +1057,15 @@ render_kernel(const KParams* __restrict__ Pg) {
           // Rect-only scenes, branch-free: the plane axis of the hit kind selects (o_a, d_a); the
           // hit point re-derives t = (k - o_a) / d_a as the reference does (:103) and
           // the normal is the axis, oriented against the ray (:123,:166,:209).
-          const bool kxy = kind == SPT_RECT_XY, kxz = kind == SPT_RECT_XZ, kyz = !kxy && !kxz;
+          bool kxy, kxz;
+          if constexpr (TP::CONSTGEO) {  // the axis from the position (intersect_scene)
+            kxy = hpos < kCornellNXY;
+            kxz = !kxy && hpos < kCornellNXY + kCornellNXZ;
+          } else {
+            kxy = kind == SPT_RECT_XY;
+            kxz = kind == SPT_RECT_XZ;
+          }
+          const bool kyz = !kxy && !kxz;
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
           const float n_ = H.w1 - oa;
@@ -1261,10 +1277,11 @@ render_kernel(const KParams* __restrict__ Pg) {
           const float tl = ea ? t : plane_t(kl - o.y, ia_hit);
           // (computed for every resolving lane: a branch around it cost exec-mask SALU)
           const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
-          const float w = lh ? wl : 1.0f;
-          T = mk(T.x * w, T.y * w, T.z * w);
+          // the black light ends a path that reaches it, so only the light vertex's L needs T*w
+          // (a lane whose shadow ray is blocked keeps T: the cosine sample follows)
+          const f3 Tw = mk(T.x * wl, T.y * wl, T.z * wl);
           const DevPrim& H = s_prims[kRefLightId];
-          const f3 Le = mk(fmaf(T.x, H.ex, L.x), fmaf(T.y, H.ey, L.y), fmaf(T.z, H.ez, L.z));
+          const f3 Le = mk(fmaf(Tw.x, H.ex, L.x), fmaf(Tw.y, H.ey, L.y), fmaf(Tw.z, H.ez, L.z));
           L = mk(lh ? Le.x : L.x, lh ? Le.y : L.y, lh ? Le.z : L.z);
           ls = lh ? kStTerm : kStCos;
         }
