@@ -521,6 +521,23 @@ def main() -> None:
         except Exception:  # noqa: BLE001
             pmc = {}
 
+    # the hardware's own count: SQ_INSTS_VALU_FLOPS_FP32 of the newest round's
+    # C3 instruction-class passes (scripts/session.sh classes) counts FP32 operations per
+    # wave-instruction; x 64 lanes x the measured lane utilisation = FLOP executed per launch
+    hw = {}
+    cls = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_c3_classes.json")))
+    if cls and args.config == "c3" and world == 1:
+        try:
+            c_ = json.load(open(cls[-1]))["counters"]
+            lu = c_["SQ_THREAD_CYCLES_VALU"] / (64.0 * c_["SQ_ACTIVE_INST_VALU"])
+            hw_flop = c_["SQ_INSTS_VALU_FLOPS_FP32"] * 64.0 * lu
+            hw = {"frac_hw": round(hw_flop / (float(kms.mean()) * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                  "hw_flop_per_launch": round(hw_flop, -6),
+                  "hw_source": f"profiles/{os.path.basename(cls[-1])}: SQ_INSTS_VALU_FLOPS_FP32 x 64 "
+                               f"x lane utilisation {lu:.3f} over this run's kernel time"}
+        except Exception:  # noqa: BLE001
+            hw = {}
+
     gather_exact = None
     if rank == 0:
         img = full.cpu().numpy()
@@ -579,6 +596,7 @@ def main() -> None:
                          # scene test (the rest are rejected exactly by the light pre-test)
                          "achieved_executed": round(achieved_x, 3),
                          "frac_executed": round(achieved_x / PEAK_FP32_TFLOPS, 4),
+                         **hw,
                          "traffic": traffic,
                          "hbm_gbs": (round(traffic / (kms.mean() * 1e-3) / 1e9, 2)
                                      if traffic else None),

@@ -9,7 +9,10 @@
 //   --mirror-glass: that box with smallpt's mirror and glass balls (pure path tracing)
 //   --spheres32: config 5's 32-sphere scene (room + light of :288-294 and 32 DIFF spheres)
 //   --devices N: row tiles sharded over GPUs 0..N-1, one RCCL gather to GPU 0 (spt_render_multi)
+//   --repeat N: render N times (spt_render keeps its device context between calls) and print
+//               each call's wall time beside its kernel time (tools/dropin_e2e.py)
 // Same scene, camera (:521), clamp/toInt and P3 output; the pixel loop is one spt_render() call.
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -24,7 +27,7 @@ int main(int argc, char* argv[]) {
   const char* out = "image.ppm";
   bool cosine = false, uniform = false, specular = false, classic = false, mirror_glass = false;
   bool spheres = false;
-  int device = 0, devices = 0, max_depth = 0, npos = 0, format = SPT_IMAGE_P3;
+  int device = 0, devices = 0, max_depth = 0, npos = 0, format = SPT_IMAGE_P3, repeat = 1;
   float q = -1.0f;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--cos")) cosine = true;
@@ -37,6 +40,7 @@ int main(int argc, char* argv[]) {
     else if (!std::strcmp(argv[i], "--q") && i + 1 < argc) q = (float)std::atof(argv[++i]);
     else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--devices") && i + 1 < argc) devices = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--repeat") && i + 1 < argc) repeat = std::max(1, std::atoi(argv[++i]));
     else if (!std::strcmp(argv[i], "--p6")) format = SPT_IMAGE_P6;
     else if (!std::strcmp(argv[i], "--pfm")) format = SPT_IMAGE_PFM;
     else if (npos < 4) pos[npos++] = std::atoi(argv[i]);
@@ -60,22 +64,31 @@ int main(int argc, char* argv[]) {
                                         : specular ? cornell_specular_scene()
                                         : spheres ? spheres32_scene()
                                                   : cornell_scene();
-    if (devices > 0) {
-      std::vector<int32_t> devs(devices);
-      for (int k = 0; k < devices; ++k) devs[k] = k;
-      c = render_multi(scene, cam, p, devs, &st);
-    } else {
-      c = render(scene, cam, p, &st);
+    for (int k = 0; k < repeat; ++k) {
+      const auto c0 = std::chrono::high_resolution_clock::now();
+      if (devices > 0) {
+        std::vector<int32_t> devs(devices);
+        for (int j = 0; j < devices; ++j) devs[j] = j;
+        c = render_multi(scene, cam, p, devs, &st);
+      } else {
+        c = render(scene, cam, p, &st);
+      }
+      const auto c1 = std::chrono::high_resolution_clock::now();
+      if (repeat > 1)
+        std::cout << "CALL " << k << " : WALL_MS " << std::chrono::duration<double, std::milli>(c1 - c0).count()
+                  << "  KERNEL_MS " << st.kernel_ms << std::endl;
     }
   } catch (const std::exception& e) {
     std::cerr << "render failed: " << e.what() << std::endl;
     return 1;
   }
+  const auto w0 = std::chrono::high_resolution_clock::now();
   if (write_ppm(out, p.width, p.height, c.data(), device, format)) {
     std::cerr << "cannot write " << out << ": " << spt_last_error() << std::endl;
     return 1;
   }
   const auto t2 = std::chrono::high_resolution_clock::now();
+  std::cout << "WRITE_MS : " << std::chrono::duration<double, std::milli>(t2 - w0).count() << std::endl;
   const double samples = (double)p.width * p.height * p.spp;
   std::cout << "KERNEL_MS : " << st.kernel_ms << "  MSAMPLES/S : " << samples / (st.kernel_ms * 1e3)
             << "  VERTICES/SAMPLE : " << (double)st.vertices / samples << std::endl;
