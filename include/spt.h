@@ -197,7 +197,10 @@ spt_status spt_context_reserve(spt_context* ctx, int32_t n_prims, const spt_para
 spt_status spt_render_async(spt_context* ctx, const spt_prim* prims, int32_t n_prims,
                             const spt_camera* cam, const spt_params* p, float* rgb_dev,
                             void* stream);
-/* Synchronises the context's last render and returns its stats. */
+/* Synchronises the context's last render and returns its stats (SPT_ERR_INVALID_ARG before the
+ * context's first render).
+ * A render that hit the kernel's runaway-iteration guard returns SPT_ERR_HIP here and leaves its
+ * rgb_dev all NaN (never a partial image). */
 spt_status spt_context_stats(spt_context* ctx, spt_stats* out);
 
 /* ---- multi-GPU: row-tile shards and ONE framebuffer gather over RCCL ----
@@ -265,7 +268,8 @@ spt_status spt_encoder_destroy(spt_encoder* enc);
 /* Encode on `stream` into out_dev (cap bytes). *len_out = encoded length. P3's length depends on
  * the data, so P3 synchronises `stream` once (after its passes); P6/PFM do not. rgb_dev must be
  * 16-byte aligned (SPT_ERR_INVALID_ARG otherwise; P6/PFM also need out_dev past the header 16-byte
- * aligned). One encoder runs one encode at a time (its scratch is reused). */
+ * aligned) and 3*w*h <= 2^32 - 8192; a call rejected for its arguments queues nothing and leaves
+ * out_dev untouched. One encoder runs one encode at a time (its scratch is reused). */
 spt_status spt_encode_image(spt_encoder* enc, const float* rgb_dev, int32_t w, int32_t h,
                             int32_t format, uint8_t* out_dev, uint64_t cap, uint64_t* len_out,
                             void* stream);

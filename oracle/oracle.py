@@ -119,6 +119,17 @@ def plane_k(k: float) -> float:
     return float(np.float32(L.spt_oracle_plane_k(k)))
 
 
+def plane_t_mismatches(num, inv) -> int:
+    """Operands (float32 arrays) on which the oracle's fast plane distance differs in its bits from
+    the contract's fma(n, inv, -2^-149) (spt_oracle_plane_t_mismatches)."""
+    num = np.ascontiguousarray(num, dtype=np.float32)
+    inv = np.ascontiguousarray(inv, dtype=np.float32)
+    L = lib()
+    L.spt_oracle_plane_t_mismatches.restype = ctypes.c_int
+    L.spt_oracle_plane_t_mismatches.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    return int(L.spt_oracle_plane_t_mismatches(num.ctypes.data, inv.ctypes.data, len(num)))
+
+
 def counter_render(prims, cam, params, rows=None, threads: int = 0):
     """Counter-mode contract on the CPU. Returns ((nrows, w, 3) float32, stats dict)."""
     if rows is None:

@@ -761,12 +761,12 @@ static void c_find_room(c_ctx* C, const spt_prim* s) {
 }
 
 /* Contract v5: the nearest-hit key of a candidate at t on the plane (or sphere) with grouped
- * position pos: the float bits of t minus one (so 0 < t < tmin stays ONE unsigned compare, +-0,
- * negatives, inf and NaN rank last) with the low 6 bits replaced by pos. The nearest hit is the
- * smallest key: a candidate's t is ranked to 64 ulps, ties and near-ties inside that resolve to
- * the lower position (the reference: strict `<` over rect[] :328, ties to the lower index). On the
- * GPU a key is one v_add and one v_bitop3, and the running minimum one v_min_u32 -- no compare and
- * lane-mask select per candidate. */
+ * position pos: the float bits of t with the low 6 bits replaced by pos, so an unsigned minimum
+ * ranks the candidates (negatives -- a plane's zero distance is -2^-149, c_plane_t, a sphere
+ * without a root -0 -- and NaN rank last; kKeyNone = tmin 1e20 of :324). A candidate's t is
+ * ranked to 64 ulps; ties and near-ties inside that resolve to the lower position (the reference:
+ * strict `<` over rect[] :328, ties to the lower index). On the GPU a key is one v_bitop3 and the
+ * running minimum one v_min_u32 -- no compare and lane-mask select per candidate. */
 static inline uint32_t c_key(float t, int pos) { return (asu(t) | 63u) ^ (uint32_t)(63 - pos); }
 #define C_KEY_NONE (asu(1e20f) | 63u) /* tmin = 1e20 (:324): no hit */
 /* A plane's distance in contract v5: t = (k - o_a) * inv_a as one fma with -2^-149 added. That is
@@ -774,7 +774,35 @@ static inline uint32_t c_key(float t, int pos) { return (asu(t) | 63u) ^ (uint32
  * and turns a zero distance (the origin on the plane: :106 `t<0`, :328 `d != 0` reject it) into
  * -2^-149, which ranks last like every negative t: the key needs no "minus one" to put +0 last. */
 #define C_NEG_TINY (-0x1p-149f)
-static inline float c_plane_t(float n, float inv) { return fmaf(n, inv, C_NEG_TINY); }
+static inline float c_plane_t_fma(float n, float inv) { return fmaf(n, inv, C_NEG_TINY); }
+/* The same value without the fma's denormal addend (an x86 microcode assist of ~100+ cycles per
+ * call: it made this restatement 10x slower). The product p = n * inv is exact in double. For a
+ * normal p the fma rounds p - 2^-149, which can differ from round(p) only when p lies exactly
+ * midway between two floats (p is a multiple of a 2^-46-relative unit, so nothing else lies within
+ * 2^-149 of a midpoint): the fma then returns the lower neighbour. p == 0 gives -2^-149; tiny and
+ * huge p (float denormal range, overflow) and NaN take the fma itself. Checked against
+ * c_plane_t_fma on constructed ties and random operands (spt_oracle_plane_t_mismatches). */
+static inline float c_plane_t(float n, float inv) {
+  const double p = (double)n * (double)inv;
+  const double ap = fabs(p);
+  float r, lo;
+  if (!(ap >= 0x1p-125 && ap <= 0x1p127)) return p == 0.0 ? C_NEG_TINY : c_plane_t_fma(n, inv);
+  r = (float)p; /* normal, nonzero: its neighbours are one step of the bit pattern away */
+  lo = (double)r > p ? asf(p > 0.0 ? asu(r) - 1u : asu(r) + 1u) : r;
+  return (double)lo != p && p - (double)lo == (double)asf(p > 0.0 ? asu(lo) + 1u : asu(lo) - 1u) - p ? lo : r;
+}
+/* Test hook: how many of the n (num[i], inv[i]) give different bits from the fma form. */
+int spt_oracle_plane_t_mismatches(const float* num, const float* inv, int n) {
+  int i, bad = 0;
+  for (i = 0; i < n; i++) {
+    const float a = c_plane_t(num[i], inv[i]), b = c_plane_t_fma(num[i], inv[i]);
+    uint32_t ua, ub;
+    memcpy(&ua, &a, 4);
+    memcpy(&ub, &b, 4);
+    bad += ua != ub;
+  }
+  return bad;
+}
 static inline uint32_t c_umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 /* The counter-mode scene intersection (intersect :323-335). inv = rcp_nr(d) once per ray.

@@ -2,7 +2,7 @@
 # PMC passes (one counter group per run) on the encoder microbench (tools/bench_image.py 4096^2).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+mkdir -p gpurun_out gpurun_out/enc_pmc
 export TMPDIR=/tmp
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \

@@ -2,7 +2,7 @@
 # Measurement session on the GPU box (in-tree build): GPU tests, the C3 rocprofv3 session (kernel
 # trace + separate PMC passes, scripts/profile.sh), instruction-class PMC passes, and the bench lines
 # of every config (C2-C5, with their CPU baselines). Outputs are tagged with TAG (default r04).
-#   PARTS="pytest smoke rehearsal profile classes bench" selects parts; each GPU step has its own time limit and the
+#   PARTS="pytest smoke rehearsal profile classes dropin bench" selects parts; each GPU step has its own time limit and the
 #   script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -21,7 +21,7 @@ if has smoke; then
   rc=$?; echo "smoke exit $rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has rehearsal; then  # the N>1 bench path on the one GPU (gloo gather; RCCL needs one GPU per rank)
-  RANKS="${RANKS:-2 4}" bash scripts/rehearsal_r02.sh || exit $?
+  RANKS="${RANKS:-2 4}" bash scripts/rehearsal.sh || exit $?
 fi
 if has profile; then
   bash scripts/profile.sh $TAG || exit $?
@@ -46,6 +46,14 @@ if has classes; then
     done
     python3 scripts/pmc_summary.py gpurun_out/cls_$cfg > gpurun_out/cls_$cfg/summary.json
   done
+fi
+if has dropin; then  # the drop-in program end to end (tools/dropin_e2e.py) and its kernels under rocprofv3
+  timeout -k 10 600 python tools/dropin_e2e.py --ref-spp 8 --out gpurun_out/${TAG}_dropin.json \
+    > gpurun_out/dropin.log 2>&1
+  rc=$?; echo "dropin exit $rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/dropin.log; exit $rc; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_dropin -o dropin \
+    -- small-pathtracer_amd/smallpt_amd 1024 768 512 1 /tmp/dropin.ppm --repeat 3 > gpurun_out/prof_dropin.log 2>&1
+  rc=$?; echo "dropin rocprof exit $rc"; [ $rc -eq 0 ] || exit $rc
 fi
 if has bench; then
   for cfg in c3 c2 c4 c5; do

@@ -472,13 +472,19 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
                                        int32_t format, uint8_t* out_dev, uint64_t cap,
                                        uint64_t* len_out, void* stream_v) {
   if (!e || !rgb_dev || !out_dev || !len_out) return img_fail(SPT_ERR_INVALID_ARG, "null argument");
-  if (w <= 0 || h <= 0 || (uint64_t)w * (uint64_t)h > 0xFFFFFFFFull / 3)
+  // 3 w h <= 2^32 - 8192: the text kernels' 32-bit value index of the last block cannot wrap
+  if (w <= 0 || h <= 0 || 3ull * (uint64_t)w * (uint64_t)h > 0xFFFFFFFFull - kTxtBlockVals)
     return img_fail(SPT_ERR_INVALID_ARG, "bad image size");
   if (format < SPT_IMAGE_P3 || format > SPT_IMAGE_PFM) return img_fail(SPT_ERR_INVALID_ARG, "bad format");
+  const std::string hd = header(w, h, format);
+  // every argument check before any work is queued: a rejected call leaves out_dev and the
+  // encoder's scratch as they were
+  if (((uintptr_t)rgb_dev & 15u) != 0) return img_fail(SPT_ERR_INVALID_ARG, "framebuffer must be 16-byte aligned");
+  if (format != SPT_IMAGE_P3 && ((uintptr_t)(out_dev + hd.size()) & 15u) != 0)
+    return img_fail(SPT_ERR_INVALID_ARG, "output raster must be 16-byte aligned");
   IMG_HIP(hipSetDevice(e->device));
   hipStream_t stream = (hipStream_t)stream_v;
   const uint32_t n_pix = (uint32_t)((uint64_t)w * (uint64_t)h);
-  const std::string hd = header(w, h, format);
   const Thresholds& T = thresholds();
   uint64_t len;
   if (format == SPT_IMAGE_P3) {
@@ -499,8 +505,6 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
       e->scratch_cap = need;
       e->epoch = 0;
     }
-    if (((uintptr_t)rgb_dev & 15u) != 0)
-      return img_fail(SPT_ERR_INVALID_ARG, "framebuffer must be 16-byte aligned");
     const uint32_t epoch = ++e->epoch == 0 ? ++e->epoch : e->epoch;  // never 0 (the initial word)
     uint64_t* offs = (uint64_t*)(e->scratch + off_b);
     uint32_t* blen = (uint32_t*)(e->scratch + len_b);
@@ -532,8 +536,6 @@ extern "C" spt_status spt_encode_image(spt_encoder* e, const float* rgb_dev, int
     const uint32_t nv = n_pix * 3;
     // grid-stride loops over ~8 blocks per CU (the block prologue stages the toInt table)
     const uint32_t grid = std::max(1u, std::min((nv / 4 + kThreads - 1) / kThreads, 2048u));
-    if (((uintptr_t)rgb_dev & 15u) || ((uintptr_t)(out_dev + hd.size()) & 15u))
-      return img_fail(SPT_ERR_INVALID_ARG, "framebuffer and output must be 16-byte aligned");
     if (format == SPT_IMAGE_P6) {
       hipLaunchKernelGGL(p6_write, dim3(grid), dim3(kThreads), 0, stream, (const float4*)rgb_dev, nv, T,
                          (uint32_t*)(out_dev + hd.size()), (uint32_t*)nullptr, 0u);

@@ -306,8 +306,9 @@ __device__ __forceinline__ Ray6 ray6(f3 o, f3 d, float ix, float iy, float iz) {
 // replaced by pos (negatives, inf and NaN rank last; a plane's zero distance is -2^-149, plane_t,
 // and a sphere without a root -0); the nearest hit is the smallest key. Per candidate that is one
 // v_bitop3 and one v_min_u32 -- where rounds 1-4 compared keys and selected (t, position) through
-// lane masks, a v_cmp -> s_and -> two v_cndmask chain per test: C3 13.55 -> 12.75 ms, and the
-// fma'd -2^-149 that spares the key's "minus one" ... (A/B, profiles/r04_ab.txt).
+// lane masks, a v_cmp -> s_and -> two v_cndmask chain per test. With the rest of contract v5 C3
+// 13.55 -> 12.75 ms, and the fma'd -2^-149 below (no "minus one" before the key) 12.92 -> 12.42 ms
+// on a slower box (A/B, profiles/r04_ab.txt sessions 2-4).
 // A parallel pair's candidate is the smaller of its two planes' keys (the smaller positive t: the
 // plane the rounds-1-4 pair rule chose); its in-plane test is evaluated at that plane's t. The
 // winner's exact t is recomputed by whoever needs it (shading, NEE weight) from its plane or
@@ -389,11 +390,34 @@ __device__ __forceinline__ void room_accept(uint32_t rk, f3 o, f3 d, float mx, f
   const bool inb = (bool)((int)(fabsf(ax) <= hx) & (int)(fabsf(ay) <= hy) & (int)(fabsf(az) <= hz));
   tmin = umin(tmin, inb ? rk : 0xFFFFFFFFu);
 }
+#ifndef SPT_BOXSLAB
+#define SPT_BOXSLAB 0
+#endif
+constexpr bool is_box_test(int J) {
+  return SPT_BOXSLAB && (J == 1 || J == 2 || J == 5 || J == 6 || J == 8 || J == 9);
+}
 template <int J>
 __device__ __forceinline__ void cornell_test(const Ray6* rays, uint32_t& tmin) {
   constexpr CTest T = kCornellTests.t[J];
-  if constexpr (J != kCornellRoom[0] && J != kCornellRoom[1] && J != kCornellRoom[2])
+  if constexpr (J != kCornellRoom[0] && J != kCornellRoom[1] && J != kCornellRoom[2] && !is_box_test(J))
     rect_cand<J, T.pos0 != T.pos1>(CornellTestPtr<J>{}, rays[T.axis], tmin);
+}
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+template <int JZ, int JX, int JT>
+__device__ __forceinline__ void box_slab(const Ray6* rays, uint32_t& tmin) {
+  constexpr CTest Z = kCornellTests.t[JZ], X = kCornellTests.t[JX], T = kCornellTests.t[JT];
+  constexpr CTest F = kCornellTests.t[kCornellRoom[1]];  // Bottom/Top: the floor is its k0
+  const Ray6 &rz = rays[2], &ry = rays[1], &rx = rays[0];
+  const int kx0 = (int)key_c<X.pos0>(plane_t(X.k0 - rx.oa, rx.ia));
+  const int kx1 = (int)key_c<X.pos1>(plane_t(X.k1 - rx.oa, rx.ia));
+  const int kz0 = (int)key_c<Z.pos0>(plane_t(Z.k0 - rz.oa, rz.ia));
+  const int kz1 = (int)key_c<Z.pos1>(plane_t(Z.k1 - rz.oa, rz.ia));
+  const int ky1 = (int)key_c<T.pos0>(plane_t(T.k0 - ry.oa, ry.ia));
+  const int ky0 = (int)key_c<F.pos0>(plane_t(F.k0 - ry.oa, ry.ia));
+  const int en = imax(imax(imin(kx0, kx1), imin(kz0, kz1)), imin(ky0, ky1));
+  const int ex = imin(imin(imax(kx0, kx1), imax(kz0, kz1)), imax(ky0, ky1));
+  tmin = umin(tmin, en <= ex ? (uint32_t)en : 0xFFFFFFFFu);
 }
 template <int... J>
 __device__ __forceinline__ void cornell_tests(std::integer_sequence<int, J...>, const Ray6* rays,
@@ -511,6 +535,10 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     constexpr CRoom B = kCornellRoomDef;
     room_accept(rk, o, d, B.box[0], B.box[1], B.box[2], B.box[3], B.box[4], B.box[5], tmin);
     cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);
+    if constexpr (SPT_BOXSLAB) {
+      box_slab<1, 8, 5>(rays, tmin);
+      box_slab<2, 9, 6>(rays, tmin);
+    }
   } else {
     const int ntxy = n_of<TP>(TP::NTXY, G->n_txy), ntxz = n_of<TP>(TP::NTXZ, G->n_txz);
     const int ntyz = n_of<TP>(TP::NTYZ, G->n_tyz);
@@ -529,14 +557,19 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   (void)rect;
   if constexpr (TP::SPH) {
     const int nsph = G->n_sph, nnar = nsph - G->n_sph_wide, base = G->n_xy + G->n_xz + G->n_yz;
-#ifndef SPT_SPH_UNROLL
-#define SPT_SPH_UNROLL 4
-#endif
-    // unrolled so the scalar loads of several spheres are issued before one wait; 4, not 8: the
-    // 32 SGPRs of 8 spheres pushed the SGPR-capped sphere kernel to 65 VGPRs (7 waves/SIMD);
-    // at 4 it has 63 (8 waves): C5 at 256 spp 475 -> 467 ms
-#pragma unroll SPT_SPH_UNROLL
-    for (int j = 0; j < nnar; ++j) tmin = umin(tmin, key_s(sphere_t(sphs[j], o, d), (uint32_t)(base + j)));
+    // unrolled by 4 so the scalar loads of several spheres are issued before one wait; 4, not 8:
+    // the 32 SGPRs of 8 spheres pushed the SGPR-capped sphere kernel to 65 VGPRs (7 waves/SIMD);
+    // at 4 it has 63 (8 waves): C5 at 256 spp 475 -> 467 ms. By hand, remainder first: the key's
+    // inline asm is convergent, and LLVM does not runtime-unroll a loop that holds convergent code.
+    auto sph_key = [&](int j) { tmin = umin(tmin, key_s(sphere_t(sphs[j], o, d), (uint32_t)(base + j))); };
+    int j = 0;
+    for (; j < (nnar & 3); ++j) sph_key(j);
+    for (; j < nnar; j += 4) {
+      sph_key(j);
+      sph_key(j + 1);
+      sph_key(j + 2);
+      sph_key(j + 3);
+    }
     if constexpr (TP::WIDE) {
       for (int j = nnar; j < nsph; ++j)  // wide spheres (fp64)
         tmin = umin(tmin, key_s(sphere_t_wide(G->sphd[j], o, d), (uint32_t)(base + j)));
@@ -1430,10 +1463,15 @@ finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict_
 __global__ void __launch_bounds__(kBlock)
 finalize_slots_kernel(const unsigned long long* __restrict__ accum,
                       const unsigned long long* __restrict__ slots, float* __restrict__ rgb,
-                      uint32_t npix, uint32_t n_chunks, uint32_t scr_k, uint32_t scr_q) {
+                      uint32_t npix, uint32_t n_chunks, uint32_t scr_k, uint32_t scr_q,
+                      const unsigned long long* __restrict__ stats) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= npix) return;
   const uint32_t p = (t & ((1u << scr_k) - 1u)) * scr_q + (t >> scr_k);
+  if (stats[0] != 0) {  // the launch hit its iteration cap: the slots of the units it dropped hold an
+    rgb[3ull * p] = rgb[3ull * p + 1] = rgb[3ull * p + 2] = __builtin_nanf("");  // earlier launch's
+    return;                                                                  // sums; no image at all
+  }
   unsigned long long v0 = accum[3ull * p], v1 = accum[3ull * p + 1], v2 = accum[3ull * p + 2];
   for (uint32_t j = 0; j < n_chunks; ++j) {
     const unsigned long long* q = slots + 3ull * ((size_t)j * npix + t);
@@ -1499,6 +1537,7 @@ struct spt_context {
   unsigned long long* h_stats = nullptr;
   hipEvent_t ev2 = nullptr;
   bool pending = false;
+  bool launched = false;  // a render has been enqueued (spt_context_stats has events to read)
   int n_prims = 0;
   KParams last{};
   // Pinned staging for the async scene upload; reused only after the previous upload completed.
@@ -1777,6 +1816,7 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipEventCreate(&c->ev2);
   if (e == hipSuccess) e = hipHostMalloc(&c->h_stats, sizeof(unsigned long long) * kStatWords, hipHostMallocDefault);
+  if (e == hipSuccess) std::memset(c->h_stats, 0, sizeof(unsigned long long) * kStatWords);  // stats before any launch: zeros
   if (e != hipSuccess) {
     spt_context_destroy(c);
     return fail(SPT_ERR_OOM, std::string("context alloc: ") + hipGetErrorString(e));
@@ -1870,6 +1910,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                            hipMemcpyDeviceToHost, stream));
     SPT_HIP(hipEventRecord(c->ev2, stream));
     c->pending = true;
+    c->launched = true;
     return SPT_OK;
   }
   K.n_local_pix = rows * p->width;
@@ -2066,7 +2107,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const uint32_t np = (uint32_t)K.n_local_pix;
   hipLaunchKernelGGL(finalize_slots_kernel, dim3((np + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
                      (const unsigned long long*)c->accum, (const unsigned long long*)c->slots,
-                     rgb_dev, np, (uint32_t)n_chunks, K.scr_k, K.scr_q);
+                     rgb_dev, np, (uint32_t)n_chunks, K.scr_k, K.scr_q,
+                     (const unsigned long long*)c->stats);
 #else
   const uint32_t n = 3u * (uint32_t)K.n_local_pix;
   hipLaunchKernelGGL(finalize_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
@@ -2077,11 +2119,13 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                          hipMemcpyDeviceToHost, stream));
   SPT_HIP(hipEventRecord(c->ev2, stream));
   c->pending = true;
+  c->launched = true;
   return SPT_OK;
 }
 
 extern "C" spt_status spt_context_stats(spt_context* c, spt_stats* out) {
   if (!c || !out) return fail(SPT_ERR_INVALID_ARG, "null argument");
+  if (!c->launched) return fail(SPT_ERR_INVALID_ARG, "no render has been enqueued on this context");
   SPT_HIP(hipSetDevice(c->device));
   SPT_HIP(hipEventSynchronize(c->ev2));
   const unsigned long long* h = c->h_stats;

@@ -118,3 +118,28 @@ def test_encoder_reuse_across_nan_and_clean_images(spt, oracle):
             assert bytes(out[:n].cpu().numpy()) == oracle.encode_image(img, 0)
     finally:
         enc.close()
+
+
+@pytest.mark.parametrize("name,fmt", FMTS)
+def test_unaligned_framebuffer_rejected_before_any_work(spt, oracle, name, fmt):
+    """A framebuffer that is not 16-byte aligned is refused (SPT_ERR_INVALID_ARG) before anything is
+    queued: the output buffer keeps its bytes, and the same Encoder then encodes correctly."""
+    import torch
+    h, w = 4, 5
+    rgb = np.random.default_rng(3).random((h, w, 3), dtype=np.float32)
+    buf = torch.zeros(h * w * 3 + 4, dtype=torch.float32, device="cuda")
+    buf[1:1 + h * w * 3].copy_(torch.from_numpy(rgb.reshape(-1)))
+    cap = spt.Encoder.bound(w, h, name)
+    out = torch.full((cap,), 0xAB, dtype=torch.uint8, device="cuda")
+    enc = spt.Encoder(0)
+    try:
+        with pytest.raises(spt.SptError, match="aligned"):
+            enc.encode(buf.data_ptr() + 4, w, h, name, out.data_ptr(), cap)
+        torch.cuda.synchronize()
+        assert bool((out == 0xAB).all())
+        src = torch.from_numpy(np.ascontiguousarray(rgb)).cuda()
+        n = enc.encode(src.data_ptr(), w, h, name, out.data_ptr(), cap)
+        torch.cuda.synchronize()
+        assert bytes(out[:n].cpu().numpy()) == oracle.encode_image(rgb, fmt)
+    finally:
+        enc.close()

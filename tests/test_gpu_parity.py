@@ -434,3 +434,14 @@ def test_dropin_render_reuses_its_context(spt, oracle):
             spt.shutdown()
     spt.shutdown()
     spt.shutdown()  # idempotent
+
+
+def test_context_stats_before_any_render_is_an_error(spt):
+    """spt_context_stats on a fresh context has no render to report: SPT_ERR_INVALID_ARG, not the
+    pinned buffer's uninitialised words (include/spt.h)."""
+    r = spt.Renderer(0)
+    try:
+        with pytest.raises(spt.SptError, match="no render"):
+            r.stats()
+    finally:
+        r.close()

@@ -285,6 +285,28 @@ def test_counter_mode_thread_invariance(oracle):
     assert np.array_equal(a, b) and sa == sb
 
 
+def test_fast_plane_distance_equals_the_fma(oracle):
+    """The oracle computes the contract's plane distance fma(n, inv, -2^-149) without the fma's
+    denormal addend (an x86 assist that made it 10x slower): same bits on exact rounding ties
+    (where the fma picks the lower neighbour), zeros, signs, infinities, NaN, tiny and huge
+    products, and random operands."""
+    f32 = np.float32
+    rng = np.random.default_rng(11)
+    # exact ties: (1 + 2^-12 m)(1 + 2^-12 m') has its 2^-24 bit as the only bit below the ulp
+    m = np.arange(1, 200, dtype=np.float64)
+    a = (1 + m * 2.0 ** -12).astype(f32)
+    ties_n = np.concatenate([a, -a, a * f32(2 ** 20), a * f32(2 ** -20), -a * f32(3)])
+    ties_i = np.concatenate([a, a, a, a, a])
+    special = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-30, 1e-38, 3e38, 1e-45],
+                       dtype=f32)
+    sn, si = np.meshgrid(special, special)
+    rn = (rng.standard_normal(200000) * rng.choice([1e-3, 1, 1e3], 200000)).astype(f32)
+    ri = (1 / rng.standard_normal(200000)).astype(f32)
+    num = np.concatenate([ties_n, sn.ravel(), rn])
+    inv = np.concatenate([ties_i, si.ravel(), ri])
+    assert oracle.plane_t_mismatches(num, inv) == 0
+
+
 def test_plane_k_rule(oracle):
     """Contract plane coordinates (spt_oracle_plane_k; kernel spt_cornell.h plane_k): fp32-exact
     values stay; otherwise the neighbouring float with the double's last significand bit."""
