@@ -119,6 +119,19 @@ def plane_k(k: float) -> float:
     return float(np.float32(L.spt_oracle_plane_k(k)))
 
 
+def scene_boxes(prims, params) -> int:
+    """Boxes of contract v6 that the oracle finds in the scene (spt_oracle_scene_boxes)."""
+    arr = (_spt.spt_prim * len(prims))(*prims)
+    L = lib()
+    L.spt_oracle_scene_boxes.restype = ctypes.c_int
+    return int(L.spt_oracle_scene_boxes(arr, len(prims), ctypes.byref(params)))
+
+
+def set_boxes(on: bool) -> None:
+    """Test hook: False = boxes tested face by face (pairs and a top), True = the contract."""
+    lib().spt_oracle_set_boxes(int(bool(on)))
+
+
 def plane_t_mismatches(num, inv) -> int:
     """Operands (float32 arrays) on which the oracle's fast plane distance differs in its bits from
     the contract's fma(n, inv, -2^-149) (spt_oracle_plane_t_mismatches)."""

@@ -627,6 +627,9 @@ typedef struct {
   int light_pos;        /* grouped position of P->light_id (-1: none) */
   int room[3];          /* tests of the scene's room (c_find_room), -1 = none */
   float room_m[3], room_h[3]; /* room box per axis x, y, z: mid and half + 2^-8 */
+  int n_box;            /* boxes standing on the room's floor (c_find_boxes) */
+  int box[21][3];       /* their tests: XY pair (planes z), YZ pair (planes x), XZ top */
+  unsigned char in_box[64]; /* test index -> 1 if it is part of a box */
   int unit;     /* c_unit_dirs: 1 = unit directions, 0 = the free-scale contract */
   float nee_c;  /* free-scale NEE weight constant: light_area / pi, rounded once */
 } c_ctx;
@@ -651,6 +654,7 @@ static int c_unit_dirs(const spt_prim* s, int n) {
 }
 static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T);
 static void c_find_room(c_ctx* C, const spt_prim* s);
+static void c_find_boxes(c_ctx* C, const spt_prim* s);
 static int g_unit_override = -1; /* test hook: -1 = the contract (c_unit_dirs), 0/1 = forced */
 void spt_oracle_set_unit_dirs(int mode) { g_unit_override = mode; }
 static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n, const spt_params* P,
@@ -669,6 +673,7 @@ static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n,
         if (CP[i].kind == SPT_SPHERE && CP[i].wide == kind) C->pos2idx[pos++] = i;
   }
   c_find_room(C, prims);
+  c_find_boxes(C, prims);
   {
     int i;
     C->light_pos = -1;
@@ -687,6 +692,9 @@ static int g_pairs = 1;
 /* Test hook: 0 = no pairing (every rectangle tested on its own: the per-rectangle form the pair
  * rule must reproduce), 1 = the contract. Not thread-safe against a running render. */
 void spt_oracle_set_pairs(int on) { g_pairs = on != 0; }
+/* Test hook: 0 = boxes tested face by face (as pairs and a top), 1 = the contract (c_find_boxes). */
+static int g_boxes = 1;
+void spt_oracle_set_boxes(int on) { g_boxes = on != 0; }
 static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T) {
   int used[64] = {0}, gpos[64], nt = 0, kind, i, j, g = 0;
   for (kind = SPT_RECT_XY; kind <= SPT_RECT_YZ; kind++)
@@ -760,6 +768,57 @@ static void c_find_room(c_ctx* C, const spt_prim* s) {
   }
 }
 
+/* Contract v6 (round 4): a BOX is a parallel XY pair, a parallel YZ pair and a single XZ top (not
+ * the light, none of them the room's) that close an axis-aligned box standing on the room's floor:
+ * the YZ planes are the x bounds of the XY pair and of the top, the XY planes the z bounds of the
+ * YZ pair and of the top, both pairs span y from the floor plane (the room's lower XZ plane) to
+ * the top's plane, and the floor's bounds contain the box's footprint -- compared on the caller's
+ * doubles. The reference's two boxes (:298-308) qualify. Found in test order, each test used once.
+ * c_intersect tests a box as one slab candidate (the faces' in-plane compares are gone); the
+ * bottom is the floor plane, reported as the floor. */
+static void c_find_boxes(c_ctx* C, const spt_prim* s) {
+  int a, b, c, used[64] = {0};
+  double floor_k, gf[4];
+  C->n_box = 0;
+  memset(C->in_box, 0, sizeof C->in_box);
+  if (!g_pairs || !g_boxes || C->room[0] < 0) return;
+  {
+    const c_test* F = &C->tests[C->room[1]];
+    floor_k = s[F->id0].geom[4] < s[F->id1].geom[4] ? s[F->id0].geom[4] : s[F->id1].geom[4];
+    memcpy(gf, s[F->id0].geom, sizeof gf); /* floor bounds: x (0, 1), z (2, 3) */
+  }
+  for (a = 0; a < C->n_tests; a++) {
+    const c_test* A = &C->tests[a]; /* XY pair: bounds x (geom 0,1), y (2,3); planes z */
+    if (A->kind != SPT_RECT_XY || A->id0 == A->id1 || a == C->room[0] || used[a]) continue;
+    for (b = 0; b < C->n_tests; b++) {
+      const c_test* D = &C->tests[b]; /* YZ pair: bounds y (0,1), z (2,3); planes x */
+      if (D->kind != SPT_RECT_YZ || D->id0 == D->id1 || b == C->room[2] || used[b]) continue;
+      for (c = 0; c < C->n_tests; c++) {
+        const c_test* T = &C->tests[c]; /* XZ single: bounds x (0,1), z (2,3); plane y */
+        const double *ga = s[A->id0].geom, *gd = s[D->id0].geom, *gt;
+        double xa, xb, za, zb;
+        if (T->kind != SPT_RECT_XZ || T->id0 != T->id1 || T->id0 == C->P->light_id || used[c]) continue;
+        gt = s[T->id0].geom;
+        if (!c_same_range(s[D->id0].geom[4], s[D->id1].geom[4], ga[0], ga[1]) ||
+            !c_same_range(s[D->id0].geom[4], s[D->id1].geom[4], gt[0], gt[1]) ||
+            !c_same_range(s[A->id0].geom[4], s[A->id1].geom[4], gd[2], gd[3]) ||
+            !c_same_range(s[A->id0].geom[4], s[A->id1].geom[4], gt[2], gt[3]) ||
+            !c_same_range(floor_k, gt[4], ga[2], ga[3]) || !c_same_range(floor_k, gt[4], gd[0], gd[1]) ||
+            !(gt[4] > floor_k))
+          continue;
+        xa = ga[0]; xb = ga[1]; za = gd[2]; zb = gd[3];
+        if (!(gf[0] <= xa && xb <= gf[1] && gf[2] <= za && zb <= gf[3])) continue;
+        used[a] = used[b] = used[c] = 1;
+        C->in_box[a] = C->in_box[b] = C->in_box[c] = 1;
+        C->box[C->n_box][0] = a; C->box[C->n_box][1] = b; C->box[C->n_box][2] = c;
+        C->n_box++;
+        break;
+      }
+      if (used[a]) break;
+    }
+  }
+}
+
 /* Contract v5: the nearest-hit key of a candidate at t on the plane (or sphere) with grouped
  * position pos: the float bits of t with the low 6 bits replaced by pos, so an unsigned minimum
  * ranks the candidates (negatives -- a plane's zero distance is -2^-149, c_plane_t, a sphere
@@ -804,6 +863,8 @@ int spt_oracle_plane_t_mismatches(const float* num, const float* inv, int n) {
   return bad;
 }
 static inline uint32_t c_umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+static inline int32_t c_imin(int32_t a, int32_t b) { return a < b ? a : b; }
+static inline int32_t c_imax(int32_t a, int32_t b) { return a > b ? a : b; }
 
 /* The counter-mode scene intersection (intersect :323-335). inv = rcp_nr(d) once per ray.
  * The rect tests (c_build_tests) run in their contract order — kind XY, XZ, YZ — then the spheres
@@ -908,6 +969,38 @@ void spt_oracle_proof_check(int on, float y0) {
   g_proof_y0 = y0;
   g_proof_n = g_proof_bad = 0;
 }
+/* Test hook: the contract's nearest hit for n rays (o, d: 3 floats each) in the scene; t_out = 1e20
+ * and id_out = -1 on a miss. */
+static void c_prims_from_spt(const spt_prim* s, int n, c_prim* P);
+static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id);
+int spt_oracle_intersect_batch(const spt_prim* prims, int n, const spt_params* P, const float* o,
+                               const float* d, int nrays, float* t_out, int32_t* id_out) {
+  c_prim CP[64];
+  c_test CT[64];
+  c_ctx C;
+  int r;
+  if (n < 1 || n > 64) return -1;
+  c_prims_from_spt(prims, n, CP);
+  c_ctx_init(&C, prims, CP, n, P, CT);
+  for (r = 0; r < nrays; r++) {
+    int id = -1;
+    float t;
+    c_intersect(&C, fv3(o[3 * r], o[3 * r + 1], o[3 * r + 2]), fv3(d[3 * r], d[3 * r + 1], d[3 * r + 2]), &t, &id);
+    t_out[r] = t;
+    id_out[r] = id;
+  }
+  return 0;
+}
+/* Test hook: the number of contract-v6 boxes c_find_boxes finds in the scene (-1: bad input). */
+int spt_oracle_scene_boxes(const spt_prim* prims, int n, const spt_params* P) {
+  c_prim CP[64];
+  c_test CT[64];
+  c_ctx C;
+  if (n < 1 || n > 64) return -1;
+  c_prims_from_spt(prims, n, CP);
+  c_ctx_init(&C, prims, CP, n, P, CT);
+  return C.n_box;
+}
 void spt_oracle_proof_counts(uint64_t out[2]) {
   out[0] = g_proof_n;
   out[1] = g_proof_bad;
@@ -939,7 +1032,7 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     const c_test* T = &C->tests[i];
     float oa, ia, tb, a, b;
     uint32_t kp;
-    const int room = i == C->room[0] || i == C->room[1] || i == C->room[2];
+    const int room = i == C->room[0] || i == C->room[1] || i == C->room[2] || C->in_box[i];
     switch (T->kind) {
       case SPT_RECT_XY: oa = o.z; ia = iz; break;
       case SPT_RECT_XZ: oa = o.y; ia = iy; break;
@@ -980,6 +1073,27 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
       if (fabsf(ax) <= C->room_h[0] && fabsf(ay) <= C->room_h[1] && fabsf(az) <= C->room_h[2])
         tmin = c_umin(tmin, rk);
     }
+  }
+  /* Boxes (contract v6): per axis the keys of the two planes as signed integers -- for t >= 0 the
+   * integer order is the order of t, and every negative t is a negative integer -- the slab
+   * interval [min, max] (y: the floor and the top); the entry is the largest interval start, the
+   * exit the smallest interval end, and the box is crossed iff entry <= exit. Its candidate is the
+   * entry, or the exit when the origin lies inside the box (a negative entry): the face the ray
+   * leaves through, as the per-face test finds it (a vertex rounded into a box self-hits its face,
+   * like the reference's). As unsigned keys that is min(entry, exit); an exit behind the origin is
+   * negative and ranks last. */
+  for (i = 0; i < C->n_box; i++) {
+    const c_test *Z = &C->tests[C->box[i][0]], *X = &C->tests[C->box[i][1]], *Y = &C->tests[C->box[i][2]];
+    const c_test* F = &C->tests[C->room[1]];
+    const int32_t kx0 = (int32_t)c_key(c_plane_t(X->k0 - o.x, ix), X->pos0);
+    const int32_t kx1 = (int32_t)c_key(c_plane_t(X->k1 - o.x, ix), X->pos1);
+    const int32_t kz0 = (int32_t)c_key(c_plane_t(Z->k0 - o.z, iz), Z->pos0);
+    const int32_t kz1 = (int32_t)c_key(c_plane_t(Z->k1 - o.z, iz), Z->pos1);
+    const int32_t ky0 = (int32_t)c_key(c_plane_t(F->k0 - o.y, iy), F->pos0);
+    const int32_t ky1 = (int32_t)c_key(c_plane_t(Y->k0 - o.y, iy), Y->pos0);
+    const int32_t en = c_imax(c_imax(c_imin(kx0, kx1), c_imin(kz0, kz1)), c_imin(ky0, ky1));
+    const int32_t ex = c_imin(c_imin(c_imax(kx0, kx1), c_imax(kz0, kz1)), c_imax(ky0, ky1));
+    if (en <= ex) tmin = c_umin(tmin, c_umin((uint32_t)en, (uint32_t)ex));
   }
   /* Spheres: narrow (fp32) ones, then the wide (fp64) ones, each in index order (their positions) */
   for (i = C->n_rect; i < C->n; i++) {

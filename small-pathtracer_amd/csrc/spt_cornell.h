@@ -162,4 +162,54 @@ static_assert(kCornellRoom[0] == 0 && kCornellRoom[1] == 3 && kCornellRoom[2] ==
 static_assert(kCornellRoomDef.box[0] == 50.0f && kCornellRoomDef.box[1] == 49.0f + 0x1p-8f &&
                   kCornellRoomDef.box[5] == 85.0f + 0x1p-8f, "HEAD room box");
 
+// The boxes of contract v6 (oracle c_find_boxes): an XY pair, a YZ pair and an XZ top (none of
+// them the room's, the top not the light) closing a box that stands on the room's floor and lies
+// inside its bounds, compared on the constructor's doubles; searched in test order. HEAD: the tall
+// and the short box (:298-308).
+struct CBoxes { int n; int t[4][3]; };  // tests: XY pair (planes z), YZ pair (planes x), XZ top
+constexpr CBoxes cornell_boxes() {
+  CBoxes B{};
+  const CTestList& L = kCornellTests;
+  bool used[17] = {};
+  const CRect& F0 = kCornellRects[L.t[kCornellRoom[1]].pos0];  // the floor: the room's lower XZ plane
+  const CRect& F1 = kCornellRects[L.t[kCornellRoom[1]].pos1];
+  const double floor_k = F0.kd < F1.kd ? F0.kd : F1.kd;
+  for (int a = 0; a < L.n; ++a) {
+    const CTest& A = L.t[a];
+    if (A.axis != 2 || A.pos0 == A.pos1 || a == kCornellRoom[0] || used[a]) continue;
+    for (int b = 0; b < L.n && !used[a]; ++b) {
+      const CTest& D = L.t[b];
+      if (D.axis != 0 || D.pos0 == D.pos1 || b == kCornellRoom[2] || used[b]) continue;
+      for (int c = 0; c < L.n; ++c) {
+        const CTest& T = L.t[c];
+        if (T.axis != 1 || T.pos0 != T.pos1 || T.pos0 == kCornellLightPos || used[c]) continue;
+        const CRect &A0 = kCornellRects[A.pos0], &A1 = kCornellRects[A.pos1];
+        const CRect &D0 = kCornellRects[D.pos0], &D1 = kCornellRects[D.pos1], &T0 = kCornellRects[T.pos0];
+        if (!same_range(D0.kd, D1.kd, A0.a1, A0.a2) || !same_range(D0.kd, D1.kd, T0.a1, T0.a2) ||
+            !same_range(A0.kd, A1.kd, D0.b1, D0.b2) || !same_range(A0.kd, A1.kd, T0.b1, T0.b2) ||
+            !same_range(floor_k, T0.kd, A0.b1, A0.b2) || !same_range(floor_k, T0.kd, D0.a1, D0.a2) ||
+            !(T0.kd > floor_k))
+          continue;
+        if (!(F0.a1 <= A0.a1 && A0.a2 <= F0.a2 && F0.b1 <= D0.b1 && D0.b2 <= F0.b2)) continue;
+        used[a] = used[b] = used[c] = true;
+        B.t[B.n][0] = a; B.t[B.n][1] = b; B.t[B.n][2] = c;
+        ++B.n;
+        break;
+      }
+    }
+  }
+  return B;
+}
+constexpr CBoxes kCornellBoxes = cornell_boxes();
+static_assert(kCornellBoxes.n == 2 && kCornellBoxes.t[0][0] == 1 && kCornellBoxes.t[0][1] == 8 &&
+                  kCornellBoxes.t[0][2] == 5 && kCornellBoxes.t[1][0] == 2 &&
+                  kCornellBoxes.t[1][1] == 9 && kCornellBoxes.t[1][2] == 6,
+              "HEAD boxes: tall (z 32/62, x 12/42, top 50), short (z 63/88, x 63/88, top 25)");
+constexpr bool cornell_in_box(int j) {
+  for (int b = 0; b < kCornellBoxes.n; ++b)
+    for (int r = 0; r < 3; ++r)
+      if (kCornellBoxes.t[b][r] == j) return true;
+  return false;
+}
+
 }  // namespace spt

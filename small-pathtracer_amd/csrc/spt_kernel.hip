@@ -137,7 +137,7 @@ struct SceneGeo {
   int n_txy, n_txz, n_tyz, n_sph_wide;  // rect tests per kind; wide spheres = the last n_sph_wide
   // contract v5's room (oracle c_find_room): its three pair tests follow the per-kind lists in
   // test[] (XY, XZ, YZ); box = mid, half + 2^-8 for x, y, z
-  int has_room, pad_[3];
+  int has_room, n_box, pad_[2];  // n_box: boxes of contract v6 (their tests follow the room's)
   float room_box[6], pad2_[2];
   GeoRect rect[kMaxPrims];  // [0,n_xy) XY, [n_xy, n_xy+n_xz) XZ, then YZ
   GeoSph sph[kMaxPrims];
@@ -217,8 +217,10 @@ struct CornellRectPtr {
 // specialisations are all-DIFF, cosine-scatter scenes (keeps their cosine block branch-free).
 // NT*: rect tests per kind (parallel pairs count once).
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false,
-          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_, bool WIDE_ = false>
+          int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_, bool WIDE_ = false,
+          int NBOX_ = -1>
 struct Topo {
+  static constexpr int NBOX = NBOX_;  // boxes of contract v6 (uploaded geometry; -1 = run time)
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
   static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
@@ -230,7 +232,7 @@ struct Topo {
 };
 // rect[] of :287-311 (light = XZ #3 -> pos 8); tests besides the room (contract v5): 2 XY box
 // pairs; light + 2 box tops; 2 YZ box pairs
-using TopoCornell = Topo<6, 5, 6, false, 8, false, 2, 3, 2>;
+using TopoCornell = Topo<6, 5, 6, false, 8, false, 0, 1, 0, false, false, 2>;
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 // Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
@@ -390,34 +392,54 @@ __device__ __forceinline__ void room_accept(uint32_t rk, f3 o, f3 d, float mx, f
   const bool inb = (bool)((int)(fabsf(ax) <= hx) & (int)(fabsf(ay) <= hy) & (int)(fabsf(az) <= hz));
   tmin = umin(tmin, inb ? rk : 0xFFFFFFFFu);
 }
-#ifndef SPT_BOXSLAB
-#define SPT_BOXSLAB 0
-#endif
-constexpr bool is_box_test(int J) {
-  return SPT_BOXSLAB && (J == 1 || J == 2 || J == 5 || J == 6 || J == 8 || J == 9);
-}
 template <int J>
 __device__ __forceinline__ void cornell_test(const Ray6* rays, uint32_t& tmin) {
   constexpr CTest T = kCornellTests.t[J];
-  if constexpr (J != kCornellRoom[0] && J != kCornellRoom[1] && J != kCornellRoom[2] && !is_box_test(J))
+  if constexpr (J != kCornellRoom[0] && J != kCornellRoom[1] && J != kCornellRoom[2] && !cornell_in_box(J))
     rect_cand<J, T.pos0 != T.pos1>(CornellTestPtr<J>{}, rays[T.axis], tmin);
 }
+// A box of contract v6 (oracle c_find_boxes / c_intersect): an XY pair Z (planes z), a YZ pair X
+// (planes x) and an XZ top, standing on the room's floor F (the room's XZ pair, k0). Per axis the two
+// planes' keys as signed integers -- for t >= 0 the integer order is the order of t, and every
+// negative t is a negative integer -- give the slab interval [min, max]; entry = the largest start,
+// exit = the smallest end, crossed iff entry <= exit. The candidate is the entry, or for an origin
+// inside the box (negative entry) the exit face, as the per-face tests find it: as unsigned keys
+// min(entry, exit). Per box 6 plane keys, 8 integer min/max, one compare: the 4 faces' and the top's
+// in-plane compares and lane-mask selects are gone (trace 153 -> 131 VALU per wave-iteration).
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
-template <int JZ, int JX, int JT>
-__device__ __forceinline__ void box_slab(const Ray6* rays, uint32_t& tmin) {
-  constexpr CTest Z = kCornellTests.t[JZ], X = kCornellTests.t[JX], T = kCornellTests.t[JT];
-  constexpr CTest F = kCornellTests.t[kCornellRoom[1]];  // Bottom/Top: the floor is its k0
-  const Ray6 &rz = rays[2], &ry = rays[1], &rx = rays[0];
-  const int kx0 = (int)key_c<X.pos0>(plane_t(X.k0 - rx.oa, rx.ia));
-  const int kx1 = (int)key_c<X.pos1>(plane_t(X.k1 - rx.oa, rx.ia));
-  const int kz0 = (int)key_c<Z.pos0>(plane_t(Z.k0 - rz.oa, rz.ia));
-  const int kz1 = (int)key_c<Z.pos1>(plane_t(Z.k1 - rz.oa, rz.ia));
-  const int ky1 = (int)key_c<T.pos0>(plane_t(T.k0 - ry.oa, ry.ia));
-  const int ky0 = (int)key_c<F.pos0>(plane_t(F.k0 - ry.oa, ry.ia));
+__device__ __forceinline__ void box_keys(int kx0, int kx1, int kz0, int kz1, int ky0, int ky1,
+                                         uint32_t& tmin) {
   const int en = imax(imax(imin(kx0, kx1), imin(kz0, kz1)), imin(ky0, ky1));
   const int ex = imin(imin(imax(kx0, kx1), imax(kz0, kz1)), imax(ky0, ky1));
-  tmin = umin(tmin, en <= ex ? (uint32_t)en : 0xFFFFFFFFu);
+  tmin = umin(tmin, en <= ex ? umin((uint32_t)en, (uint32_t)ex) : 0xFFFFFFFFu);
+}
+template <int B>
+__device__ __forceinline__ void cornell_box(const Ray6* rays, uint32_t& tmin) {
+  constexpr CTest Z = kCornellTests.t[kCornellBoxes.t[B][0]], X = kCornellTests.t[kCornellBoxes.t[B][1]];
+  constexpr CTest T = kCornellTests.t[kCornellBoxes.t[B][2]], F = kCornellTests.t[kCornellRoom[1]];
+  const Ray6 &rz = rays[2], &ry = rays[1], &rx = rays[0];
+  box_keys((int)key_c<X.pos0>(plane_t(X.k0 - rx.oa, rx.ia)), (int)key_c<X.pos1>(plane_t(X.k1 - rx.oa, rx.ia)),
+           (int)key_c<Z.pos0>(plane_t(Z.k0 - rz.oa, rz.ia)), (int)key_c<Z.pos1>(plane_t(Z.k1 - rz.oa, rz.ia)),
+           (int)key_c<F.pos0>(plane_t(F.k0 - ry.oa, ry.ia)), (int)key_c<T.pos0>(plane_t(T.k0 - ry.oa, ry.ia)),
+           tmin);
+}
+template <int... B>
+__device__ __forceinline__ void cornell_boxes(std::integer_sequence<int, B...>, const Ray6* rays,
+                                              uint32_t& tmin) {
+  (cornell_box<B>(rays, tmin), ...);
+}
+// The same for uploaded geometry: bx[0] the XY pair, bx[1] the YZ pair, bx[2] the top, fl the
+// room's XZ pair (its k0 the floor)
+template <class GT>
+__device__ __forceinline__ void geo_box(GT bx, GT fl, const Ray6& rz, const Ray6& ry, const Ray6& rx,
+                                        uint32_t& tmin) {
+  box_keys((int)key_v(plane_t(bx[1].k0 - rx.oa, rx.ia), (uint32_t)bx[1].pos0),
+           (int)key_v(plane_t(bx[1].k1 - rx.oa, rx.ia), (uint32_t)bx[1].pos1),
+           (int)key_v(plane_t(bx[0].k0 - rz.oa, rz.ia), (uint32_t)bx[0].pos0),
+           (int)key_v(plane_t(bx[0].k1 - rz.oa, rz.ia), (uint32_t)bx[0].pos1),
+           (int)key_v(plane_t(fl->k0 - ry.oa, ry.ia), (uint32_t)fl->pos0),
+           (int)key_v(plane_t(bx[2].k0 - ry.oa, ry.ia), (uint32_t)bx[2].pos0), tmin);
 }
 template <int... J>
 __device__ __forceinline__ void cornell_tests(std::integer_sequence<int, J...>, const Ray6* rays,
@@ -535,20 +557,19 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     constexpr CRoom B = kCornellRoomDef;
     room_accept(rk, o, d, B.box[0], B.box[1], B.box[2], B.box[3], B.box[4], B.box[5], tmin);
     cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);
-    if constexpr (SPT_BOXSLAB) {
-      box_slab<1, 8, 5>(rays, tmin);
-      box_slab<2, 9, 6>(rays, tmin);
-    }
+    cornell_boxes(std::make_integer_sequence<int, kCornellBoxes.n>{}, rays, tmin);
   } else {
     const int ntxy = n_of<TP>(TP::NTXY, G->n_txy), ntxz = n_of<TP>(TP::NTXZ, G->n_txz);
     const int ntyz = n_of<TP>(TP::NTYZ, G->n_tyz);
     const Ray6 rz = ray6<2>(o, d, ix, iy, iz), ry = ray6<1>(o, d, ix, iy, iz), rx = ray6<0>(o, d, ix, iy, iz);
-    if (G->has_room) {  // wave-uniform; the room tests follow the per-kind lists
+    if (G->has_room) {  // wave-uniform; the room tests follow the per-kind lists, then the boxes
       const int nt = ntxy + ntxz + ntyz;
       const uint32_t rk = umin(umin(room_pair<0>(tests + nt, rz), room_pair<0>(tests + nt + 1, ry)),
                                room_pair<0>(tests + nt + 2, rx));
       room_accept(rk, o, d, G->room_box[0], G->room_box[1], G->room_box[2], G->room_box[3],
                   G->room_box[4], G->room_box[5], tmin);
+      const int nbox = n_of<TP>(TP::NBOX, G->n_box);
+      for (int b = 0; b < nbox; ++b) geo_box(tests + nt + 3 + 3 * b, tests + nt + 1, rz, ry, rx, tmin);
     }
     test_group<TP::NTXY>(tests, ntxy, rz, tmin);
     test_group<TP::NTXZ>(tests + ntxy, ntxz, ry, tmin);
@@ -802,7 +823,7 @@ render_kernel(const KParams* __restrict__ Pg) {
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
       s_prims[i] = P->prims[i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
-      if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz + 3 * G->has_room) {
+      if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz + 3 * G->has_room + 3 * G->n_box) {
         const SPT_CONST GeoTest& q = G->test[i];
         s_test[i] = GeoTest{q.k0, q.k1, q.ma, q.ha, q.mb, q.hb, q.pos0, q.pos1};
       }
@@ -1729,6 +1750,60 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
       --g->n_txy; --g->n_txz; --g->n_tyz;
     }
   }
+  // Contract v6's boxes (oracle c_find_boxes): an XY pair, a YZ pair and an XZ top (not the light)
+  // closing a box on the room's floor, inside the floor's bounds, in the caller's doubles; searched
+  // in test order. Their tests move behind the room's, three per box (XY pair, YZ pair, top).
+  if (g->has_room) {
+    const int nt = g->n_txy + g->n_txz + g->n_tyz;
+    auto member = [&](int pos) -> const spt_prim& { return s[g->rect[pos].idx]; };
+    auto same_range = [](double k1, double k2, double b1, double b2) {
+      return std::min(k1, k2) == b1 && std::max(k1, k2) == b2;
+    };
+    const GeoTest& F = g->test[nt + 1];
+    const double floor_k = std::min(member(F.pos0).geom[4], member(F.pos1).geom[4]);
+    const double* gf = member(F.pos0).geom;
+    bool used[kMaxPrims] = {};
+    int box[kMaxPrims / 5][3], nb = 0;
+    for (int a = 0; a < g->n_txy; ++a) {
+      const GeoTest& A = g->test[a];
+      if (A.pos0 == A.pos1 || used[a]) continue;
+      for (int b = g->n_txy + g->n_txz; b < nt && !used[a]; ++b) {
+        const GeoTest& D = g->test[b];
+        if (D.pos0 == D.pos1 || used[b]) continue;
+        for (int c = g->n_txy; c < g->n_txy + g->n_txz; ++c) {
+          const GeoTest& T = g->test[c];
+          if (T.pos0 != T.pos1 || T.pos0 == *light_pos || used[c]) continue;
+          const double *ga = member(A.pos0).geom, *gd = member(D.pos0).geom, *gt = member(T.pos0).geom;
+          const double xA = gd[4], xB = member(D.pos1).geom[4], zA = ga[4], zB = member(A.pos1).geom[4];
+          if (!same_range(xA, xB, ga[0], ga[1]) || !same_range(xA, xB, gt[0], gt[1]) ||
+              !same_range(zA, zB, gd[2], gd[3]) || !same_range(zA, zB, gt[2], gt[3]) ||
+              !same_range(floor_k, gt[4], ga[2], ga[3]) || !same_range(floor_k, gt[4], gd[0], gd[1]) ||
+              !(gt[4] > floor_k))
+            continue;
+          if (!(gf[0] <= ga[0] && ga[1] <= gf[1] && gf[2] <= gd[2] && gd[3] <= gf[3])) continue;
+          used[a] = used[b] = used[c] = true;
+          box[nb][0] = a; box[nb][1] = b; box[nb][2] = c;
+          ++nb;
+          break;
+        }
+      }
+    }
+    if (nb > 0) {
+      GeoTest rest[kMaxPrims];
+      int n = 0, kind_n[3] = {0, 0, 0};
+      for (int i = 0; i < nt; ++i) {
+        if (used[i]) continue;
+        rest[n++] = g->test[i];
+        ++kind_n[i < g->n_txy ? 0 : (i < g->n_txy + g->n_txz ? 1 : 2)];
+      }
+      for (int r = 0; r < 3; ++r) rest[n + r] = g->test[nt + r];  // the room
+      for (int b = 0; b < nb; ++b)
+        for (int r = 0; r < 3; ++r) rest[n + 3 + 3 * b + r] = g->test[box[b][r]];
+      for (int i = 0; i < n + 3 + 3 * nb; ++i) g->test[i] = rest[i];
+      g->n_txy = kind_n[0]; g->n_txz = kind_n[1]; g->n_tyz = kind_n[2];
+      g->n_box = nb;
+    }
+  }
   // Spheres in index order, the narrow (fp32) ones first, then the wide (fp64) ones (oracle
   // c_intersect): the kernel's fp32 loop carries no per-sphere precision test.
   for (int pass = 0; pass < 2; ++pass)
@@ -1772,6 +1847,13 @@ static bool cornell_const_match(const SceneGeo& g, int light_pos) {
       if (g.test[nt + r].pos0 != C.pos0 || g.test[nt + r].pos1 != C.pos1) return false;
     }
     if (std::memcmp(g.room_box, kCornellRoomDef.box, sizeof g.room_box) != 0) return false;
+    if (g.n_box != kCornellBoxes.n) return false;  // and the same boxes (their tests behind the room's)
+    for (int b = 0; b < kCornellBoxes.n; ++b)
+      for (int r = 0; r < 3; ++r) {
+        const CTest& C = kCornellTests.t[kCornellBoxes.t[b][r]];
+        const GeoTest& T = g.test[nt + 3 + 3 * b + r];
+        if (T.pos0 != C.pos0 || T.pos1 != C.pos1) return false;
+      }
   }
   for (int i = 0; i < kCornellNXY + kCornellNXZ + kCornellNYZ; ++i) {
     const GeoRect& R = g.rect[i];
@@ -1931,7 +2013,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                                                         : 3;
   const bool cornell = kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER) &&
                        g.n_xy == 6 && g.n_xz == 5 && g.n_yz == 6 && g.n_sph == 0 && light_pos == 8 &&
-                       g.n_txy == 2 && g.n_txz == 3 && g.n_tyz == 2 && g.has_room;
+                       g.n_txy == 0 && g.n_txz == 1 && g.n_tyz == 0 && g.has_room && g.n_box == 2;
   const bool cconst = cornell && kcap >= 2 && cornell_const_match(g, light_pos);
   // Estimator specialisations of the HEAD-geometry kernel (Cfg): the reference's own settings.
   // axis-aligned camera (Cfg CAMAX): horizontal.y/z and vertical.x/z zero, origin nonzero

@@ -401,6 +401,51 @@ def _random_scene(spt, rng, n_rect, n_sph, mats):
     return prims
 
 
+def _box_scene(spt, boxes, spheres=0, seed=0):
+    """The reference's room and light (:287-294) plus axis-aligned white boxes, each as the
+    reference builds its two (:298-308): two XY faces, two YZ faces and an XZ top. boxes: (x0, x1,
+    z0, z1, y0, y1); y0 = 0 stands on the floor (a box of contract v6), y0 > 0 floats (its faces are
+    tested one by one). Optional DIFF spheres above the boxes."""
+    prims = list(spt.cornell_scene())[:7]
+
+    def rect(kind, a1, a2, b1, b2, k):
+        p = spt.spt_prim()
+        p.kind = kind
+        p.geom[:] = [a1, a2, b1, b2, k]
+        p.c[:] = [1.0, 1.0, 1.0]
+        return p
+    for x0, x1, z0, z1, y0, y1 in boxes:
+        prims += [rect(0, x0, x1, y0, y1, z0), rect(0, x0, x1, y0, y1, z1),
+                  rect(2, y0, y1, z0, z1, x0), rect(2, y0, y1, z0, z1, x1),
+                  rect(1, x0, x1, z0, z1, y1)]
+    rng = np.random.default_rng(seed)
+    for _ in range(spheres):
+        p = spt.spt_prim()
+        p.kind = spt.SPHERE
+        p.geom[:] = [4.0, float(rng.uniform(10, 90)), float(rng.uniform(60, 75)),
+                     float(rng.uniform(20, 150)), 0.0]
+        p.c[:] = [0.7, 0.7, 0.7]
+        prims.append(p)
+    return prims
+
+
+BOXES3 = [(10, 30, 20, 45, 0, 30), (55.5, 80.25, 100, 130, 0, 12.3), (40, 60, 60, 80, 0, 55),
+          (70, 90, 20, 40, 10, 30)]  # the last one floats
+
+
+@pytest.mark.parametrize("spheres", [0, 3])
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_box_scenes_bit_exact(spt, oracle, spheres, nee):
+    """Contract v6's boxes in uploaded geometry (the generic rect kernel and the sphere kernel):
+    three boxes standing on the floor and one floating, image and statistics equal to the oracle."""
+    prims = _box_scene(spt, BOXES3, spheres, seed=5)
+    p = spt.default_params(width=48, height=36, spp=8, seed=3, nee_prob=nee, max_depth=12)
+    assert oracle.scene_boxes(prims, p) == 3
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
 @pytest.mark.parametrize("seed,n_rect,n_sph,mats", [
     (1, 6, 0, (0,)),        # rect-only, another topology: the generic kernel, rect tests from LDS
     (2, 3, 9, (0,)),        # all-DIFF with spheres: the sphere kernel

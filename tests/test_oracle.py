@@ -217,13 +217,15 @@ def test_counter_mode_pins(oracle):
 
 @pytest.mark.parametrize("est,q", [("nee", 1.0), ("cos", 0.0)])
 def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
-    """The contract's parallel-pair rect tests (one plane of a box's opposite faces per ray) and its
-    room test (the nearest of the three wall pairs, one box check widened by 2^-8: contract v5)
-    against testing every rectangle on its own (intersect :323-335 as written). The skipped plane of
-    a pair is never the nearest hit outside ulp-level edge grazes; the room rule differs only for
-    rays from outside the room (leaked paths) that pass within 2^-8 of a wall's edge. Measured at
-    128x96, seed 7: misses 348289 vs 348488 (-0.06 %), 4 of 12288 pixels differ by <= 2.7e-4 (NEE);
-    cosine-only: 0 pixels (the leaked paths carry no light)."""
+    """The contract's parallel-pair rect tests (one plane of a box's opposite faces per ray), its
+    room test (the nearest of the three wall pairs, one box check widened by 2^-8: contract v5) and
+    its box slabs (contract v6) against testing every rectangle on its own (intersect :323-335 as
+    written). The skipped plane of a pair is never the nearest hit outside ulp-level edge grazes;
+    the room rule differs only for rays from outside the room (leaked paths) that pass within 2^-8
+    of a wall's edge; a box slab differs from its five faces only for rays grazing an edge within
+    rounding (0 of 382k random rays and 168k rays from box-face vertices, self-hits included).
+    Measured at 128x96, seed 7 (NEE): 7 of 12288 pixels differ, each by one sample's worth
+    (<= 4.3e-3 at 128 spp), path rays 6788367 vs 6788388; cosine-only: misses -0.06 %."""
     prims = oracle.scene_cornell()
     p = oracle.default_params(width=128, height=96, spp=128 if est == "nee" else 64, seed=7,
                               nee_prob=q)
@@ -234,10 +236,12 @@ def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
     finally:
         oracle.set_pairs(True)
     d = np.abs(a.astype(np.float64) - b)
-    assert (d.max(axis=2) > 0).sum() <= 0.001 * d.shape[0] * d.shape[1] and d.max() < 1e-3
+    assert (d.max(axis=2) > 0).sum() <= 0.001 * d.shape[0] * d.shape[1] and d.max() <= 1.0 / p.spp
     assert sa["samples"] == sb["samples"]
     for k in ("path_rays", "vertices", "nee_light_hits", "cosine_samples", "shadow_traced"):
-        assert abs(sa[k] - sb[k]) <= 1e-5 * sa["samples"] * 10, (k, sa[k], sb[k])
+        # (one trapped path -- a vertex rounded into a white box bounces there until Russian
+        # roulette ends it -- is ~70 path rays: cosine-only, boxes on/off, 7023272 vs 7023342)
+        assert abs(sa[k] - sb[k]) <= 2e-5 * max(sa[k], sa["samples"]), (k, sa[k], sb[k])
     assert abs(sa["misses"] / sb["misses"] - 1) < 2e-3, (sa["misses"], sb["misses"])
 
 
@@ -374,3 +378,26 @@ def test_contract_fidelity_vs_reference_runs(oracle, spt, est):
     zg, z2 = fidelity.compare(fx[est], own)
     assert np.all(np.abs(zg) < fidelity.GLOBAL_Z_MAX), zg
     assert z2 < fidelity.BLOCK_Z2_MAX, z2
+
+
+def test_box_rule_finds_standing_boxes_only(oracle, spt):
+    """Contract v6 (oracle c_find_boxes): the HEAD scene's two boxes; in a scene with three boxes
+    on the floor and one floating, the three; none without pairs. Boxes on vs face by face: the
+    same image but for rays grazing an edge (here: none at 48x36 @ 8)."""
+    import test_gpu_parity as tg
+    p = oracle.default_params(width=48, height=36, spp=8, seed=3)
+    assert oracle.scene_boxes(oracle.scene_cornell(), p) == 2
+    prims = tg._box_scene(spt, tg.BOXES3)
+    assert oracle.scene_boxes(prims, p) == 3
+    oracle.set_pairs(False)
+    try:
+        assert oracle.scene_boxes(prims, p) == 0
+    finally:
+        oracle.set_pairs(True)
+    a, sa = oracle.counter_render(prims, oracle.camera(48 / 36), p)
+    oracle.set_boxes(False)
+    try:
+        b, sb = oracle.counter_render(prims, oracle.camera(48 / 36), p)
+    finally:
+        oracle.set_boxes(True)
+    assert np.array_equal(a, b) and sa == sb
