@@ -626,7 +626,6 @@ typedef struct {
   int n_rect;           /* rectangles = the first sphere's position */
   int light_pos;        /* grouped position of P->light_id (-1: none) */
   int room[3];          /* tests of the scene's room (c_find_room), -1 = none */
-  float room_m[3], room_h[3]; /* room box per axis x, y, z: mid and half + 2^-8 */
   int n_box;            /* boxes standing on the room's floor (c_find_boxes) */
   int box[21][3];       /* their tests: XY pair (planes z), YZ pair (planes x), XZ top */
   unsigned char in_box[64]; /* test index -> 1 if it is part of a box */
@@ -759,9 +758,6 @@ static void c_find_room(c_ctx* C, const spt_prim* s) {
             !c_same_range(s[A->id0].geom[4], s[A->id1].geom[4], gd[2], gd[3]))
           continue;
         C->room[0] = a; C->room[1] = b; C->room[2] = c;
-        C->room_m[0] = A->ma; C->room_h[0] = A->ha + 0x1p-8f;
-        C->room_m[1] = A->mb; C->room_h[1] = A->hb + 0x1p-8f;
-        C->room_m[2] = B->mb; C->room_h[2] = B->hb + 0x1p-8f;
         return;
       }
     }
@@ -1014,13 +1010,13 @@ void spt_oracle_proof_counts(uint64_t out[2]) {
  *    apart, far more than the keys' 64 ulps) -- and its in-plane test is evaluated at the chosen
  *    t (c_plane_t: the distance as one fma with -2^-149). Accepted iff |a| <= half and
  *    |b| <= half there (:104-106);
- *  - the ROOM (c_find_room) is one box: the smallest of its three pairs' keys is the candidate, and
- *    it is accepted iff its point at t_R = float(key) lies in the room box widened by 2^-8 on every
- *    axis. For an origin in the room the nearest of the three exit planes always lies in the box
- *    (the box is convex); the test only rejects origins outside (a leaked path), where a ray that
- *    enters the box is accepted at its entry plane and one that passes by is not. It differs from
- *    the per-wall test only within 2^-8 of a room edge (and for origins outside two of the three
- *    slabs at once), and it replaces six bounds compares by three;
+ *  - the ROOM (c_find_room) and the BOXES (c_find_boxes) are slabs (contract v6): per axis the
+ *    two planes' keys as signed integers bound the slab interval, the candidate is the entry (the
+ *    largest interval start) -- or from inside the exit face (the smallest interval end), the
+ *    nearest positive plane -- accepted iff entry <= exit. For an origin in the room that is the
+ *    wall the per-wall tests find; it differs from them only for rays grazing an edge within
+ *    rounding and it needs no in-plane compare at all (v5: the room's nearest plane accepted
+ *    within its box widened by 2^-8);
  *  - spheres: key(t, position) of the nearest root beyond the epsilon (0 = no root, ranked last).
  * The hit's t is the winner's own t, recomputed from its plane / sphere (the same bits as in its
  * key). id is left untouched on a miss; returns 1 on hit, *t = 1e20f on a miss. */
@@ -1058,21 +1054,19 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     }
     if (fabsf(a) <= T->ha && fabsf(b) <= T->hb) tmin = c_umin(tmin, kp);
   }
-  if (C->room[0] >= 0) {
-    uint32_t rk = 0xFFFFFFFFu;
+  if (C->room[0] >= 0) { /* the room as a slab (contract v6), like a box below: from inside it is
+                           * the exit face, the nearest positive plane of the three pairs */
+    int32_t en = INT32_MIN, ex = INT32_MAX;
     int r;
     for (r = 0; r < 3; r++) {
       const c_test* T = &C->tests[C->room[r]];
       const float oa = r == 0 ? o.z : (r == 1 ? o.y : o.x), ia = r == 0 ? iz : (r == 1 ? iy : ix);
-      rk = c_umin(rk, c_umin(c_key(c_plane_t(T->k0 - oa, ia), T->pos0), c_key(c_plane_t(T->k1 - oa, ia), T->pos1)));
+      const int32_t k0 = (int32_t)c_key(c_plane_t(T->k0 - oa, ia), T->pos0);
+      const int32_t k1 = (int32_t)c_key(c_plane_t(T->k1 - oa, ia), T->pos1);
+      en = c_imax(en, c_imin(k0, k1));
+      ex = c_imin(ex, c_imax(k0, k1));
     }
-    {
-      const float tr = asf(rk);
-      const float ax = fmaf(d.x, tr, o.x - C->room_m[0]), ay = fmaf(d.y, tr, o.y - C->room_m[1]),
-                  az = fmaf(d.z, tr, o.z - C->room_m[2]);
-      if (fabsf(ax) <= C->room_h[0] && fabsf(ay) <= C->room_h[1] && fabsf(az) <= C->room_h[2])
-        tmin = c_umin(tmin, rk);
-    }
+    if (en <= ex) tmin = c_umin(tmin, c_umin((uint32_t)en, (uint32_t)ex));
   }
   /* Boxes (contract v6): per axis the keys of the two planes as signed integers -- for t >= 0 the
    * integer order is the order of t, and every negative t is a negative integer -- the slab

@@ -124,9 +124,9 @@ static_assert(kCornellTests.n == 10, "HEAD scene: 7 parallel pairs + light + 2 b
 constexpr bool same_range(double k1, double k2, double b1, double b2) {
   return (k1 < k2 ? k1 : k2) == b1 && (k1 < k2 ? k2 : k1) == b2;
 }
-struct CRoom { int t[3]; float box[6]; };  // tests (XY, XZ, YZ); mid, half + 2^-8 for x, y, z
+struct CRoom { int t[3]; };  // tests (XY, XZ, YZ)
 constexpr CRoom cornell_room() {
-  CRoom R{{-1, -1, -1}, {}};
+  CRoom R{{-1, -1, -1}};
   const CTestList& L = kCornellTests;
   for (int a = 0; a < L.n; ++a) {
     if (L.t[a].axis != 2 || L.t[a].pos0 == L.t[a].pos1) continue;
@@ -146,9 +146,6 @@ constexpr CRoom cornell_room() {
             !same_range(A0.kd, A1.kd, B0.b1, B0.b2) || !same_range(A0.kd, A1.kd, D0.b1, D0.b2))
           continue;
         R.t[0] = a; R.t[1] = b; R.t[2] = c;
-        R.box[0] = A0.ma; R.box[1] = A0.ha + 0x1p-8f;
-        R.box[2] = A0.mb; R.box[3] = A0.hb + 0x1p-8f;
-        R.box[4] = B0.mb; R.box[5] = B0.hb + 0x1p-8f;
         return R;
       }
     }
@@ -159,8 +156,6 @@ constexpr CRoom kCornellRoomDef = cornell_room();
 constexpr int kCornellRoom[3] = {kCornellRoomDef.t[0], kCornellRoomDef.t[1], kCornellRoomDef.t[2]};
 static_assert(kCornellRoom[0] == 0 && kCornellRoom[1] == 3 && kCornellRoom[2] == 7,
               "HEAD room: Front/Back, Bottom/Top, Left/Right");
-static_assert(kCornellRoomDef.box[0] == 50.0f && kCornellRoomDef.box[1] == 49.0f + 0x1p-8f &&
-                  kCornellRoomDef.box[5] == 85.0f + 0x1p-8f, "HEAD room box");
 
 // The boxes of contract v6 (oracle c_find_boxes): an XY pair, a YZ pair and an XZ top (none of
 // them the room's, the top not the light) closing a box that stands on the room's floor and lies

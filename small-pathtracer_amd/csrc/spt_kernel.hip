@@ -138,7 +138,7 @@ struct SceneGeo {
   // contract v5's room (oracle c_find_room): its three pair tests follow the per-kind lists in
   // test[] (XY, XZ, YZ); box = mid, half + 2^-8 for x, y, z
   int has_room, n_box, pad_[2];  // n_box: boxes of contract v6 (their tests follow the room's)
-  float room_box[6], pad2_[2];
+  float pad2_[8];
   GeoRect rect[kMaxPrims];  // [0,n_xy) XY, [n_xy, n_xy+n_xz) XZ, then YZ
   GeoSph sph[kMaxPrims];
   GeoSphD sphd[kMaxPrims];
@@ -375,23 +375,6 @@ __device__ __forceinline__ void rect_cand(GP g, const Ray6& r, uint32_t& tmin) {
   const bool inb = (bool)((int)(fabsf(a) <= g->ha) & (int)(fabsf(b) <= g->hb));
   tmin = umin(tmin, inb ? kp : 0xFFFFFFFFu);
 }
-// The room's pair (oracle c_intersect, the room): the smaller key of its two planes, no bounds.
-template <int J, class GP>
-__device__ __forceinline__ uint32_t room_pair(GP g, const Ray6& r) {
-  const float t0 = plane_t(g->k0 - r.oa, r.ia), t1 = plane_t(g->k1 - r.oa, r.ia);
-  uint32_t kp;
-  plane_keys<J, true>(g, t0, t1, kp);
-  return kp;
-}
-// The room as one box: the nearest of its three pairs, accepted iff the point at t_R = float(key)
-// lies in the room box widened by 2^-8 (mid m, half h + 2^-8 per axis x, y, z).
-__device__ __forceinline__ void room_accept(uint32_t rk, f3 o, f3 d, float mx, float hx, float my,
-                                            float hy, float mz, float hz, uint32_t& tmin) {
-  const float tr = __uint_as_float(rk);
-  const float ax = fmaf(d.x, tr, o.x - mx), ay = fmaf(d.y, tr, o.y - my), az = fmaf(d.z, tr, o.z - mz);
-  const bool inb = (bool)((int)(fabsf(ax) <= hx) & (int)(fabsf(ay) <= hy) & (int)(fabsf(az) <= hz));
-  tmin = umin(tmin, inb ? rk : 0xFFFFFFFFu);
-}
 template <int J>
 __device__ __forceinline__ void cornell_test(const Ray6* rays, uint32_t& tmin) {
   constexpr CTest T = kCornellTests.t[J];
@@ -414,6 +397,16 @@ __device__ __forceinline__ void box_keys(int kx0, int kx1, int kz0, int kz1, int
   const int ex = imin(imin(imax(kx0, kx1), imax(kz0, kz1)), imax(ky0, ky1));
   tmin = umin(tmin, en <= ex ? umin((uint32_t)en, (uint32_t)ex) : 0xFFFFFFFFu);
 }
+// The room of contract v6 as the same slab (from inside: the exit face, the nearest positive wall)
+__device__ __forceinline__ void cornell_room(const Ray6* rays, uint32_t& tmin) {
+  constexpr CTest Z = kCornellTests.t[kCornellRoom[0]], Y = kCornellTests.t[kCornellRoom[1]];
+  constexpr CTest X = kCornellTests.t[kCornellRoom[2]];
+  const Ray6 &rz = rays[2], &ry = rays[1], &rx = rays[0];
+  box_keys((int)key_c<X.pos0>(plane_t(X.k0 - rx.oa, rx.ia)), (int)key_c<X.pos1>(plane_t(X.k1 - rx.oa, rx.ia)),
+           (int)key_c<Z.pos0>(plane_t(Z.k0 - rz.oa, rz.ia)), (int)key_c<Z.pos1>(plane_t(Z.k1 - rz.oa, rz.ia)),
+           (int)key_c<Y.pos0>(plane_t(Y.k0 - ry.oa, ry.ia)), (int)key_c<Y.pos1>(plane_t(Y.k1 - ry.oa, ry.ia)),
+           tmin);
+}
 template <int B>
 __device__ __forceinline__ void cornell_box(const Ray6* rays, uint32_t& tmin) {
   constexpr CTest Z = kCornellTests.t[kCornellBoxes.t[B][0]], X = kCornellTests.t[kCornellBoxes.t[B][1]];
@@ -429,8 +422,18 @@ __device__ __forceinline__ void cornell_boxes(std::integer_sequence<int, B...>, 
                                               uint32_t& tmin) {
   (cornell_box<B>(rays, tmin), ...);
 }
-// The same for uploaded geometry: bx[0] the XY pair, bx[1] the YZ pair, bx[2] the top, fl the
-// room's XZ pair (its k0 the floor)
+// The same for uploaded geometry: the room (rm[0] its XY pair, rm[1] XZ, rm[2] YZ) and a box (bx[0]
+// the XY pair, bx[1] the YZ pair, bx[2] the top; fl the room's XZ pair, its k0 the floor)
+template <class GT>
+__device__ __forceinline__ void geo_room(GT rm, const Ray6& rz, const Ray6& ry, const Ray6& rx,
+                                         uint32_t& tmin) {
+  box_keys((int)key_v(plane_t(rm[2].k0 - rx.oa, rx.ia), (uint32_t)rm[2].pos0),
+           (int)key_v(plane_t(rm[2].k1 - rx.oa, rx.ia), (uint32_t)rm[2].pos1),
+           (int)key_v(plane_t(rm[0].k0 - rz.oa, rz.ia), (uint32_t)rm[0].pos0),
+           (int)key_v(plane_t(rm[0].k1 - rz.oa, rz.ia), (uint32_t)rm[0].pos1),
+           (int)key_v(plane_t(rm[1].k0 - ry.oa, ry.ia), (uint32_t)rm[1].pos0),
+           (int)key_v(plane_t(rm[1].k1 - ry.oa, ry.ia), (uint32_t)rm[1].pos1), tmin);
+}
 template <class GT>
 __device__ __forceinline__ void geo_box(GT bx, GT fl, const Ray6& rz, const Ray6& ry, const Ray6& rx,
                                         uint32_t& tmin) {
@@ -550,12 +553,7 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   if constexpr (TP::CONSTGEO) {
     const Ray6 rays[3] = {ray6<0>(o, d, ix, iy, iz), ray6<1>(o, d, ix, iy, iz),
                           ray6<2>(o, d, ix, iy, iz)};
-    constexpr int R0 = kCornellRoom[0], R1 = kCornellRoom[1], R2 = kCornellRoom[2];
-    const uint32_t rk = umin(umin(room_pair<R0>(CornellTestPtr<R0>{}, rays[kCornellTests.t[R0].axis]),
-                                  room_pair<R1>(CornellTestPtr<R1>{}, rays[kCornellTests.t[R1].axis])),
-                             room_pair<R2>(CornellTestPtr<R2>{}, rays[kCornellTests.t[R2].axis]));
-    constexpr CRoom B = kCornellRoomDef;
-    room_accept(rk, o, d, B.box[0], B.box[1], B.box[2], B.box[3], B.box[4], B.box[5], tmin);
+    cornell_room(rays, tmin);
     cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);
     cornell_boxes(std::make_integer_sequence<int, kCornellBoxes.n>{}, rays, tmin);
   } else {
@@ -564,10 +562,7 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     const Ray6 rz = ray6<2>(o, d, ix, iy, iz), ry = ray6<1>(o, d, ix, iy, iz), rx = ray6<0>(o, d, ix, iy, iz);
     if (G->has_room) {  // wave-uniform; the room tests follow the per-kind lists, then the boxes
       const int nt = ntxy + ntxz + ntyz;
-      const uint32_t rk = umin(umin(room_pair<0>(tests + nt, rz), room_pair<0>(tests + nt + 1, ry)),
-                               room_pair<0>(tests + nt + 2, rx));
-      room_accept(rk, o, d, G->room_box[0], G->room_box[1], G->room_box[2], G->room_box[3],
-                  G->room_box[4], G->room_box[5], tmin);
+      geo_room(tests + nt, rz, ry, rx, tmin);
       const int nbox = n_of<TP>(TP::NBOX, G->n_box);
       for (int b = 0; b < nbox; ++b) geo_box(tests + nt + 3 + 3 * b, tests + nt + 1, rz, ry, rx, tmin);
     }
@@ -1738,9 +1733,6 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
     g->has_room = room[0] >= 0;
     if (g->has_room) {
       const GeoTest A = g->test[room[0]], B = g->test[room[1]], D = g->test[room[2]];
-      g->room_box[0] = A.ma; g->room_box[1] = A.ha + 0x1p-8f;
-      g->room_box[2] = A.mb; g->room_box[3] = A.hb + 0x1p-8f;
-      g->room_box[4] = B.mb; g->room_box[5] = B.hb + 0x1p-8f;
       GeoTest rest[kMaxPrims];
       int n = 0;
       for (int i = 0; i < nt; ++i)
@@ -1846,7 +1838,6 @@ static bool cornell_const_match(const SceneGeo& g, int light_pos) {
       const CTest& C = kCornellTests.t[kCornellRoom[r]];
       if (g.test[nt + r].pos0 != C.pos0 || g.test[nt + r].pos1 != C.pos1) return false;
     }
-    if (std::memcmp(g.room_box, kCornellRoomDef.box, sizeof g.room_box) != 0) return false;
     if (g.n_box != kCornellBoxes.n) return false;  // and the same boxes (their tests behind the room's)
     for (int b = 0; b < kCornellBoxes.n; ++b)
       for (int r = 0; r < 3; ++r) {
