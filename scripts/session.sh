@@ -52,7 +52,7 @@ if has dropin; then  # the drop-in program end to end (tools/dropin_e2e.py) and 
     > gpurun_out/dropin.log 2>&1
   rc=$?; echo "dropin exit $rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/dropin.log; exit $rc; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_dropin -o dropin \
-    -- small-pathtracer_amd/smallpt_amd 1024 768 512 1 /tmp/dropin.ppm --repeat 3 > gpurun_out/prof_dropin.log 2>&1
+    -- small-pathtracer_amd/smallpt_amd 1024 768 512 1 /tmp/dropin.ppm --repeat 10 > gpurun_out/prof_dropin.log 2>&1
   rc=$?; echo "dropin rocprof exit $rc"; [ $rc -eq 0 ] || exit $rc
 fi
 if has bench; then
