@@ -5,7 +5,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}; shift || true
-ARGS=${*:---steps 6 --warmup 2 --no-cpu-baseline}
+# one frame in flight: every render dispatch runs alone, so the trace's average duration is the
+# isolated kernel time the bench line's roofline.kernel_ms reports (two overlapping frames stretch
+# each other's dispatch spans)
+ARGS=${*:---steps 6 --warmup 2 --no-cpu-baseline --frames-in-flight 1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 run() {  # name, rocprof args...

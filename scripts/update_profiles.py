@@ -20,7 +20,7 @@ shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"),
             os.path.join(prof, f"{rnd}_rocprof_kernel_stats.csv"))
 summ = json.loads(subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), src],
                                  check=True, capture_output=True, text=True).stdout)
-summ["session"] = f"scripts/profile.sh {tag} (bench.py c3, --steps 6 --warmup 2: 8 dispatches)"
+summ["session"] = f"scripts/profile.sh {tag} (bench.py c3, --steps 6 --warmup 2 --frames-in-flight 1)"
 json.dump(summ, open(os.path.join(prof, f"{rnd}_pmc_summary.json"), "w"), indent=1)
 c = summ["counters"]
 fetch = 2 * c["FETCH_SIZE"] * 1024
