@@ -5,6 +5,7 @@
 //   -DSPT_DIAG=2  SPT_WAVE_TIMES: per-wave start / end times, iterations and CU (s_memrealtime),
 //                 dumped to $SPT_WAVE_DUMP; tools/wave_tail.py reads it (queue tail, residency)
 // Tuning constants with an A/B history (SPT_STEAL_MIN, SPT_GRAB, SPT_SMALL_ITERS, SPT_SMALL_UNITS,
+// SPT_UNITS_PER_LANE,
 // SPT_NUM_SGPR) are plain numbers with their measured defaults in spt_kernel.hip.
 #pragma once
 #if defined(SPT_DIAG) && SPT_DIAG == 1

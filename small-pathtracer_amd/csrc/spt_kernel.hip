@@ -69,6 +69,10 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 #ifndef SPT_SMALL_UNITS
 #define SPT_SMALL_UNITS 1.5
 #endif
+// Units per resident lane of a long launch (host, spt_render_async): 8 since round 4 (was 16)
+#ifndef SPT_UNITS_PER_LANE
+#define SPT_UNITS_PER_LANE 8.0
+#endif
 #ifndef SPT_SCRAMBLE_K
 #define SPT_SCRAMBLE_K 8  // pixel-order spreading factor of the work units (1 = off; A/B in DESIGN.md §4)
 #endif
@@ -2063,9 +2067,12 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
       K.early_y0 = y0;
     }
   }
-  // Unit size: ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured
-  // 25.0 ms vs 26.0 ms at 8 units/lane and 27.8 ms at 2); never changes results (integer
-  // accumulation).
+  // Unit size: SPT_UNITS_PER_LANE (8) units per resident lane (C3: 96 samples); never changes
+  // results (integer accumulation). Round 1 chose 16 (25.0 ms vs 26.0 ms at 8 units/lane, before
+  // in-wave stealing); re-measured in round 4 with stealing, unit slots and two frames in flight
+  // (profiles/r04_ab.txt session 6, 3 rounds): bench value 35.7 / 36.1 / 36.3 / 36.4 / 36.5
+  // Gsamples/s at 48 / 64 / 80 / 96 / 112 samples per unit, isolated kernel 11.67 / 11.60 / 11.60 /
+  // 11.68 / 11.70 ms -- fewer refills and retires, and the next frame fills the longer tail.
   int chunk = p->chunk;
   const double lanes = (double)c->n_cu * c->bpc[kv] * kBlock;  // resident lanes of THIS kernel
   const double rays_per_sample = p->nee_prob > 0.0f ? 5.3 : 8.9;  // HEAD: NEE / cosine only
@@ -2079,9 +2086,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
       const double units_per_pix = std::max(1.0, std::ceil(SPT_SMALL_UNITS * lanes / std::max(1, K.n_local_pix)));
       chunk = (int)std::ceil(p->spp / units_per_pix);
     } else {
-      // ~16 units per resident lane so the queue's tail is short (C3: 48 samples; measured 25.0 ms
-      // vs 26.0 ms at 8 units/lane and 27.8 ms at 2)...
-      const double per_pix = std::max(1.0, 16.0 * lanes / std::max(1, K.n_local_pix));
+      // SPT_UNITS_PER_LANE units per resident lane (above)...
+      const double per_pix = std::max(1.0, SPT_UNITS_PER_LANE * lanes / std::max(1, K.n_local_pix));
       chunk = (int)std::max(4.0, std::ceil(p->spp / per_pix));
     }
     // ...but a unit should last >= ~200 lane-iterations: every unit costs a refill (~35 VALU +
