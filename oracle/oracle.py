@@ -89,13 +89,14 @@ def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, pri
 
     row_seed: seed erand48's row streams with the seed too (oracle/_ref/smallpt_cos_xs); without it
     the reference's scattering/RR draws are the same for every seed. stats: also return
-    {"vertices", "misses"} over all radiance() calls. qthr: the NEE-mix threshold of :464
+    {"vertices", "misses", "first_misses", "vertices_pre"} over all radiance() calls (first_misses:
+    samples whose path missed; vertices_pre: vertices up to and with a path's first miss). qthr: the NEE-mix threshold of :464
     (default 1 if nee else 0; oracle/_ref/smallpt_q05 is 0.5). max_depth: the depth cap of
     oracle/_ref/smallpt_sph16 (0 = none, the reference)."""
     prims = prims or scene_cornell()
     arr = (_spt.spt_prim * len(prims))(*prims)
     out = np.zeros((h, w, 3), dtype=np.float64)
-    st = (ctypes.c_uint64 * 2)()
+    st = (ctypes.c_uint64 * 4)()
     flags = (2 if uniform else 0) | (4 if row_seed else 0)
     if qthr is None:
         qthr = 1.0 if nee else 0.0
@@ -107,7 +108,8 @@ def compat_render(w: int, h: int, spp: int, seed: int = 1, nee: bool = True, pri
     L.spt_oracle_compat_render_ex(arr, len(prims), w, h, spp, seed, flags, qthr, max_depth,
                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), st)
     if stats:
-        return out, {"vertices": int(st[0]), "misses": int(st[1])}
+        return out, {"vertices": int(st[0]), "misses": int(st[1]), "first_misses": int(st[2]),
+                     "vertices_pre": int(st[3])}
     return out
 
 
@@ -130,6 +132,12 @@ def scene_boxes(prims, params) -> int:
 def set_boxes(on: bool) -> None:
     """Test hook: False = boxes tested face by face (pairs and a top), True = the contract."""
     lib().spt_oracle_set_boxes(int(bool(on)))
+
+
+def set_leak_end(on: bool) -> None:
+    """Test hook: False = leaked paths go on from the miss vertex as the reference's (:373-374),
+    True = the contract (c_find_leak_end: they end at their first miss)."""
+    lib().spt_oracle_set_leak_end(int(bool(on)))
 
 
 def plane_t_mismatches(num, inv) -> int:

@@ -187,6 +187,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // light" — an occlusion query without id bookkeeping.
   int light_black, light_kind, light_pos;
   int scatter_uniform;  // SPT_FLAG_UNIFORM_SCATTER
+  int leak_end;         // contract v6: a leaked path ends at its first miss (host leak_end_of)
   // Sphere NEE kernel: vertices above early_y0 (every sphere's top + 1) in the HEAD room resolve
   // their light-accepted shadow rays early (early_room_proven); +inf when the host cannot prove it
   float early_y0;
@@ -1180,7 +1181,8 @@ render_kernel(const KParams* __restrict__ Pg) {
         const bool capd = (max_depth > 0) & (depth >= max_depth);
         const bool rr = (depth > rr_depth_of<CF>(P)) | (rr_t < 0);   // p == 0
         const bool alive = (int)u16i(rl.x, rl.y) < rr_t;              // (p > 0) & (p >= 1 | u16 < p)
-        const bool term = capd | (rr & !alive);
+        // contract v6: a leaked path ends at its first miss (host leak_end_of, oracle c_find_leak_end)
+        const bool term = capd | (rr & !alive) | (!hit & (P->leak_end != 0));
         const float ip = keep(H.ip);  // == 1.0f / p, read unconditionally (no branch)
         const float fsc = rr ? ip : 1.0f;
         f = mk(f.x * fsc, f.y * fsc, f.z * fsc);
@@ -1822,6 +1824,39 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
   }
 }
 
+// Contract v6 (oracle c_find_leak_end): a leaked path ends at its first miss when the scene has a
+// room, the miss vertex (the origin, :373-374) lies strictly outside the room's box, prim 0 does
+// not emit and every emitter lies strictly inside the box -- compared on the caller's doubles.
+static int leak_end_of(const spt_prim* s, int n, const SceneGeo& g) {
+  if (!g.has_room) return 0;
+  const int nt = g.n_txy + g.n_txz + g.n_tyz;
+  double lo[3], hi[3];
+  for (int a = 0; a < 3; ++a) {  // room tests: XY pair (planes z), XZ (y), YZ (x)
+    const GeoTest& T = g.test[nt + a];
+    const double k0 = s[g.rect[T.pos0].idx].geom[4], k1 = s[g.rect[T.pos1].idx].geom[4];
+    const int ax = a == 0 ? 2 : (a == 1 ? 1 : 0);
+    lo[ax] = std::min(k0, k1);
+    hi[ax] = std::max(k0, k1);
+  }
+  if (!(0.0 < lo[0] || 0.0 > hi[0] || 0.0 < lo[1] || 0.0 > hi[1] || 0.0 < lo[2] || 0.0 > hi[2])) return 0;
+  if (s[0].e[0] != 0.0 || s[0].e[1] != 0.0 || s[0].e[2] != 0.0) return 0;
+  for (int i = 0; i < n; ++i) {
+    const double* gm = s[i].geom;
+    if (s[i].e[0] == 0.0 && s[i].e[1] == 0.0 && s[i].e[2] == 0.0) continue;
+    if (s[i].kind == SPT_SPHERE) {
+      for (int a = 0; a < 3; ++a)
+        if (!(gm[1 + a] - gm[0] > lo[a] && gm[1 + a] + gm[0] < hi[a])) return 0;
+      continue;
+    }
+    const int pa = s[i].kind == SPT_RECT_XY ? 2 : (s[i].kind == SPT_RECT_XZ ? 1 : 0);
+    const int ua = s[i].kind == SPT_RECT_YZ ? 1 : 0, va = s[i].kind == SPT_RECT_XY ? 1 : 2;
+    if (!(gm[4] > lo[pa] && gm[4] < hi[pa] && gm[0] >= lo[ua] && gm[1] <= hi[ua] && gm[2] >= lo[va] &&
+          gm[3] <= hi[va]))
+      return 0;
+  }
+  return 1;
+}
+
 static int tile_rows_of(const spt_params* p) { return p->tile_rows > 0 ? p->tile_rows : 8; }
 
 // Multiply-shift reciprocal of d for 31-bit numerators: l = ceil(log2 d), m = floor(2^(31+l)/d) + 1
@@ -2156,6 +2191,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
   K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
+  K.leak_end = leak_end_of(prims, n_prims, *c->h_geo);
   // Ray-direction contract (oracle c_unit_dirs): unit directions iff a sphere or a REFR primitive
   K.unit_dirs = 0;
   for (int i = 0; i < n_prims; ++i)
