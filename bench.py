@@ -623,7 +623,11 @@ def main() -> None:
                       "rays_traced_per_sample": round((s0["path_rays"] + s0["shadow_traced"]
                                                        - s0["shadow_proven"]) / my_samples, 4),
                       "shadow_proven_per_sample": round(s0["shadow_proven"] / my_samples, 4),
-                      "misses_per_sample": round(s0["misses"] / my_samples, 4)},
+                      # contract v6: a leaked path ends at its first miss, so every miss is a
+                      # path leaving the room (the reference re-misses from its miss vertex,
+                      # :373-374: 0.22 misses but ~0.047 leaked paths per sample at C3)
+                      "misses_per_sample": round(s0["misses"] / my_samples, 4),
+                      "misses": "first misses: leaked paths end there (contract v6, DESIGN.md §3)"},
             "quality": qual,
             "gather_equals_1gpu_render": gather_exact,
             "gather": gather_mode,

@@ -1127,7 +1127,9 @@ render_kernel(const KParams* __restrict__ Pg) {
           const float n_ = H.w1 - oa;
           const float tr = hit_plane_t(n_, da, ia_hit, plane_t(n_, ia_hit));  // the winner's t, corrected
           x = mk(keep(o.x + d.x * tr), keep(o.y + d.y * tr), keep(o.z + d.z * tr));
-          x = hit ? x : mk(0, 0, 0);  // a miss vertex is the origin (:373-374)
+          // a miss vertex is the origin (:373-374); a leaked path ending at its miss (every LREF
+          // kernel, see below) never reads it
+          if constexpr (CF::LREF != 1) x = hit ? x : mk(0, 0, 0);
           l_miss += hit ? 0u : 1u;
           const float sg = da < 0.0f ? 1.0f : -1.0f;
           nl = mk(kyz ? sg : 0.0f, kxz ? sg : 0.0f, kxy ? sg : 0.0f);
@@ -1181,8 +1183,10 @@ render_kernel(const KParams* __restrict__ Pg) {
         const bool capd = (max_depth > 0) & (depth >= max_depth);
         const bool rr = (depth > rr_depth_of<CF>(P)) | (rr_t < 0);   // p == 0
         const bool alive = (int)u16i(rl.x, rl.y) < rr_t;              // (p > 0) & (p >= 1 | u16 < p)
-        // contract v6: a leaked path ends at its first miss (host leak_end_of, oracle c_find_leak_end)
-        const bool term = capd | (rr & !alive) | (!hit & (P->leak_end != 0));
+        // contract v6: a leaked path ends at its first miss (host leak_end_of, oracle
+        // c_find_leak_end); the host launches the LREF kernels only where that rule holds
+        const bool leak = CF::LREF == 1 || P->leak_end != 0;
+        const bool term = capd | (rr & !alive) | (!hit & leak);
         const float ip = keep(H.ip);  // == 1.0f / p, read unconditionally (no branch)
         const float fsc = rr ? ip : 1.0f;
         f = mk(f.x * fsc, f.y * fsc, f.z * fsc);
@@ -2059,8 +2063,9 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const bool lref = p->rr_depth == kRefRrDepth && p->light_id == kRefLightId &&
                     p->light_x0 == kRefLx0 && p->light_dx == 36.0f && p->light_z0 == kRefLz0 &&
                     p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
+  K.leak_end = leak_end_of(prims, n_prims, g);
   const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
-                        p->rr_depth >= 1 && cam_axis && lref;
+                        p->rr_depth >= 1 && cam_axis && lref && K.leak_end;
   int kv = g.n_sph_wide > 0 ? KV_WIDE : KV_GENERIC;  // (only the wide kernel has the fp64 loop)
   if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
   else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
@@ -2068,7 +2073,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   else if (cornell) kv = KV_CORNELL;
   else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
     kv = g.n_sph == 0 ? KV_RECTDIFF
-         : kcap >= 3 && K.light_black && lref && p->nee_prob >= 1.0f &&
+         : kcap >= 3 && K.light_black && lref && K.leak_end && p->nee_prob >= 1.0f &&
                  p->light_mode == SPT_LIGHT_GLIBC_WRAP && light_pos >= 0 &&
                  prims[p->light_id].kind == SPT_RECT_XZ
              ? KV_SPHDIFF_NEE
@@ -2191,7 +2196,6 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
   K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
-  K.leak_end = leak_end_of(prims, n_prims, *c->h_geo);
   // Ray-direction contract (oracle c_unit_dirs): unit directions iff a sphere or a REFR primitive
   K.unit_dirs = 0;
   for (int i = 0; i < n_prims; ++i)
