@@ -492,3 +492,18 @@ def test_context_stats_before_any_render_is_an_error(spt):
             r.stats()
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_leak_end_off_when_the_miss_vertex_emits(spt, oracle, nee):
+    """Contract v6's leak-end rule needs a non-emitting prim 0 (a missed ray's vertex, :373-374):
+    with an emissive front wall, leaked paths go on from the miss vertex as the reference's, on the
+    run-time HEAD kernel (the LREF kernels are launched only where the rule holds) -- the image and
+    statistics still equal the oracle's, and there are more misses than leaked paths."""
+    prims = list(spt.cornell_scene())
+    prims[0].e[:] = [0.05, 0.05, 0.05]
+    p = spt.default_params(width=48, height=36, spp=8, seed=4, nee_prob=nee)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert gst["misses"] / gst["samples"] > 0.1  # the reference's repeated misses, not first ones
