@@ -84,6 +84,9 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 #ifndef SPT_STEAL_MIN
 #define SPT_STEAL_MIN 8  // unstarted samples a donor must hold (in-wave stealing; A/B in DESIGN.md §4)
 #endif
+#ifndef SPT_STEAL_MIN_SMALL
+#define SPT_STEAL_MIN_SMALL 16  // the same for short launches (C2: +2-3 %, profiles/r04_ab.txt s. 9)
+#endif
 #ifdef SPT_WAVE_TIMES
 constexpr int kStatWords = 32 + 3 * 32768;  // diagnostic: per-wave start, end, iterations
 #else
@@ -188,6 +191,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   int light_black, light_kind, light_pos;
   int scatter_uniform;  // SPT_FLAG_UNIFORM_SCATTER
   int leak_end;         // contract v6: a leaked path ends at its first miss (host leak_end_of)
+  uint32_t steal_min;   // SPT_STEAL_MIN or, for a short launch, SPT_STEAL_MIN_SMALL
   // Sphere NEE kernel: vertices above early_y0 (every sphere's top + 1) in the HEAD room resolve
   // their light-accepted shadow rays early (early_room_proven); +inf when the host cannot prove it
   float early_y0;
@@ -973,9 +977,10 @@ render_kernel(const KParams* __restrict__ Pg) {
       if (idle != 0) {
         const uint32_t cur = s + (ls == kStCam ? 0u : 1u);  // first unstarted sample
         // donors: lanes with more unstarted samples than the one they start next, and at least
-        // SPT_STEAL_MIN of them (every stolen range flushes its own sums: memory-side atomics)
+        // steal_min of them (every stolen range flushes its own sums: memory-side atomics)
+        const uint32_t smin = cptr(Pg)->steal_min;
         uint64_t dm = __ballot(ls != kStIdle && s_end > cur + (ls == kStCam ? 1u : 0u) &&
-                               s_end >= cur + (uint32_t)SPT_STEAL_MIN);
+                               s_end >= cur + smin);
         while (idle != 0 && dm != 0) {
           const int il = __builtin_ctzll(idle), dl = __builtin_ctzll(dm);
           idle &= idle - 1;
@@ -2146,6 +2151,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     K.sh_guided = (small_launch || SPT_GUIDED_ALL) ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
   }
   K.chunk = chunk;
+  K.steal_min = small_launch ? SPT_STEAL_MIN_SMALL : SPT_STEAL_MIN;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
   const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
   if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
