@@ -1774,7 +1774,7 @@ static void build_geo(const spt_prim* s, int n, SceneGeo* g, int light, int* lig
     const double* gf = member(F.pos0).geom;
     bool used[kMaxPrims] = {};
     int box[kMaxPrims / 5][3], nb = 0;
-    for (int a = 0; a < g->n_txy; ++a) {
+    for (int a = 0; a < g->n_txy && nb < kMaxPrims / 5; ++a) {  // (5 rects a box: <= 12 of them)
       const GeoTest& A = g->test[a];
       if (A.pos0 == A.pos1 || used[a]) continue;
       for (int b = g->n_txy + g->n_txz; b < nt && !used[a]; ++b) {
