@@ -285,6 +285,11 @@ constexpr uint32_t kRefLdxi = 36u, kRefLdzi = 36u;
 template <class CF> __device__ __forceinline__ int light_id_of(const SPT_CONST KParams* P) {
   if constexpr (CF::LREF == 1) return kRefLightId; else return P->light_id;
 }
+// The light's id in the kernel's primitive numbering: its grouped position in the HEAD kernels
+// (s_prims is loaded in position order there, intersect_scene), its prims[] index elsewhere
+template <class TP, class CF> __device__ __forceinline__ int light_slot_of(const SPT_CONST KParams* P) {
+  if constexpr (TP::CONSTGEO) return kCornellLightPos; else return light_id_of<CF>(P);
+}
 template <class CF> __device__ __forceinline__ int rr_depth_of(const SPT_CONST KParams* P) {
   if constexpr (CF::LREF == 1) return kRefRrDepth; else return P->rr_depth;
 }
@@ -331,6 +336,19 @@ constexpr uint32_t kKeyNone = __builtin_bit_cast(uint32_t, 1e20f) | 63u;  // tmi
 constexpr float kNegTiny = -0x1p-149f;
 __device__ __forceinline__ float plane_t(float n, float inv) { return fmaf(n, inv, kNegTiny); }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+#ifndef SPT_COUNT_ADDC
+#define SPT_COUNT_ADDC 1
+#endif
+// c += b for a per-lane event counter as ONE v_addc_co_u32 with b's lane mask as its carry-in
+// (LLVM spells c + (b ? 1 : 0) as a v_cndmask and a v_add)
+__device__ __forceinline__ void count_if(uint32_t& c, bool b) {
+#if SPT_COUNT_ADDC
+  const uint64_t m = __builtin_amdgcn_ballot_w64(b);
+  asm("v_addc_co_u32_e64 %0, vcc, 0, %0, %1" : "+v"(c) : "s"(m) : "vcc");
+#else
+  c += b ? 1u : 0u;
+#endif
+}
 // (bits(t) | 63) ^ (63 - pos) as ONE v_bitop3 (0x36 = (S0 | S2) ^ S1)
 template <int POS>
 __device__ __forceinline__ uint32_t key_c(float t) {  // compile-time position (inline constant)
@@ -553,11 +571,13 @@ __device__ __forceinline__ auto tests_of(const SPT_CONST SceneGeo* G, const GeoT
 }
 // The scene's room of contract v5 in uploaded geometry: SceneGeo.room_test[] (three GeoTests kept
 // out of the per-kind test lists) and the box (host build_geo, oracle c_find_room).
-template <class TP, class GP, class GT, class SP>
+template <class TP, bool COUNT_MISS = false, class GP, class GT, class SP>
 __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP rect, GT tests,
                                                 SP sphs, const int* pos2idx, f3 o, f3 d, int& id,
-                                                float& ia_hit, int& pos_out) {
+                                                float& ia_hit, int& pos_out, uint32_t& n_miss,
+                                                f3& inv) {
   const float ix = rcp_nr(d.x), iy = rcp_nr(d.y), iz = rcp_nr(d.z);
+  inv = mk(ix, iy, iz);
   uint32_t tmin = kKeyNone;
   if constexpr (TP::CONSTGEO) {
     const Ray6 rays[3] = {ray6<0>(o, d, ix, iy, iz), ray6<1>(o, d, ix, iy, iz),
@@ -601,6 +621,9 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     }
   }
   const bool hit = tmin < kKeyNone;
+  // COUNT_MISS: every lane's miss is a path ray's (a traced shadow ray always meets the light, whose
+  // test in the trace is the pre-test's, bit for bit): counted here, where the compare is fresh
+  if constexpr (COUNT_MISS) count_if(n_miss, tmin >= kKeyNone);
   int pos = (int)(tmin & 63u);  // (63 on a miss: a valid LDS index, the id is kept)
   // HEAD kernels: a miss reports the position of prim 0, whose id a missed path ray keeps (:373-374),
   // so the shading takes the hit's plane axis from the same two position compares as ia_hit
@@ -608,8 +631,13 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
   // 1/d of the hit rectangle's plane axis (the winner's t and its hit point, see the shading)
   const int nxy = TP::CONSTGEO ? kCornellNXY : n_of<TP>(TP::NXY, G->n_xy);
   const int nxz = TP::CONSTGEO ? kCornellNXZ : n_of<TP>(TP::NXZ, G->n_xz);
-  ia_hit = pos < nxy ? iz : (pos < nxy + nxz ? iy : ix);
-  const int idn = keep(pos2idx[pos]);  // (unconditional LDS read: no branch)
+  // (the HEAD kernels select it where it is used, from the shading's own plane-axis masks)
+  if constexpr (!TP::CONSTGEO) ia_hit = pos < nxy ? iz : (pos < nxy + nxz ? iy : ix);
+  // HEAD kernels: the kernel's primitive ids ARE the grouped positions (s_prims is loaded in that
+  // order), so no pos -> index lookup; otherwise an unconditional LDS read (no branch)
+  int idn;
+  if constexpr (TP::CONSTGEO) idn = pos;
+  else idn = keep(pos2idx[pos]);
   id = hit ? idn : id;
   pos_out = pos;
   return hit;
@@ -828,7 +856,8 @@ render_kernel(const KParams* __restrict__ Pg) {
     const SPT_CONST SceneGeo* G = cptr(P->geo);
     const int nrect = G->n_xy + G->n_xz + G->n_yz;
     for (int i = threadIdx.x; i < P->n_prims; i += kBlock) {
-      s_prims[i] = P->prims[i];
+      // HEAD geometry (every primitive a rectangle): s_prims by grouped position (kPosIds)
+      s_prims[i] = P->prims[TP::CONSTGEO ? G->rect[i].idx : i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
       if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz + 3 * G->has_room + 3 * G->n_box) {
         const SPT_CONST GeoTest& q = G->test[i];
@@ -1018,6 +1047,23 @@ render_kernel(const KParams* __restrict__ Pg) {
     }
     if (__ballot(ls != kStIdle) == 0) break;
     }
+#if defined(SPT_PRIO) && SPT_PRIO > 0
+    // A/B: wave priority against the SIMD's age-first issue order ("C2")
+    if ((iter & 31u) == 0u) {
+      uint32_t pr;
+      if (SPT_PRIO == 2 || (SPT_PRIO == 3 && exhausted)) {  // tail: most remaining work first
+        const uint32_t c = (uint32_t)__popcll(__ballot(s_end >= s + 8u && ls != kStIdle));
+        pr = exhausted ? (c >= 32u ? 3u : c >= 8u ? 2u : c >= 1u ? 1u : 0u) : 0u;
+      } else {  // rotation: the wave's age rank on its SIMD plus a phase
+        pr = ((iter >> 5) + ((blockIdx.x << 3) / gridDim.x)) & 3u;
+      }
+      pr = __builtin_amdgcn_readfirstlane(pr);
+      if (pr == 0u) __builtin_amdgcn_s_setprio(0);
+      else if (pr == 1u) __builtin_amdgcn_s_setprio(1);
+      else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(3);
+    }
+#endif
     n_cos += (uint32_t)__popcll(__ballot(ls == kStCos));
 
     // 3) generate the path ray (kStCam, kStCos, kStSpec): the cosine continuation from the last
@@ -1077,11 +1123,18 @@ render_kernel(const KParams* __restrict__ Pg) {
       { float z_ = o.x; asm volatile(".rept " SPT_XSTR(SPT_PROBE_VALU) "\n v_add_f32 %0, 1.0, %0\n .endr" : "+v"(z_)); }
 #endif
       const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
-      int id = ls == kStShadow ? vid : 0;  // intersect() leaves id untouched on a miss (:323-335)
-      float t = 0.0f, ia_hit;
+      // intersect() leaves id untouched on a miss (:323-335): a shadow ray keeps its vertex's id. The
+      // early-resolve HEAD kernel needs no vertex id: its light is black, so no vertex on the light
+      // takes a NEE sample, and a missed shadow ray's id (prim 0's) is not the light's either way.
+      int id = (!kEarlyNee && ls == kStShadow) ? vid : 0;
+      float t = 0.0f, ia_hit = 0.0f;
       int hpos;
-      bool hit = intersect_scene<TP>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), G->sph, s_pos2idx, o,
-                                     d, id, ia_hit, hpos);
+      f3 inv;  // 1/d per axis (rcp_nr), the trace's
+      // (the early-resolve kernels trace a shadow ray only when the light accepts it: it never misses)
+      bool hit = intersect_scene<TP, kEarly>(G, rects_of<TP>(G), tests_of<TP>(G, s_test), G->sph, s_pos2idx,
+                                             o, d, id, ia_hit, hpos, l_miss, inv);
+      if constexpr (TP::CONSTGEO)
+        ia_hit = hpos < kCornellNXY ? inv.z : (hpos < kCornellNXY + kCornellNXZ ? inv.y : inv.x);
 
       // 5) resolve a shadow ray: the light is reached iff the nearest hit is the light (:467). Then
       //    the light is the next vertex (shaded in the common block below, T = T*f*weight); else the
@@ -1092,9 +1145,9 @@ render_kernel(const KParams* __restrict__ Pg) {
       if (!kEarly && ls == kStShadow) {
         SPT_REGION(6);
         const SPT_CONST KParams* D = cptr(Pg);
-        const bool lh = id == light_id_of<CF>(D);
+        const bool lh = id == light_slot_of<TP, CF>(D);
         if (lh) SPT_REGION(7);
-        l_hit += lh ? 1u : 0u;
+        count_if(l_hit, lh);
         if constexpr (!TP::SPH) ++l_shadow;
         const float larea = CF::LREF == 1 ? kRefLarea : D->larea;
         const float nee_c = CF::LREF == 1 ? kRefNeeC : D->nee_c;
@@ -1131,19 +1184,21 @@ render_kernel(const KParams* __restrict__ Pg) {
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
           const float n_ = H.w1 - oa;
-          const float tr = hit_plane_t(n_, da, ia_hit, plane_t(n_, ia_hit));  // the winner's t, corrected
+          float ia = ia_hit;
+          if constexpr (TP::CONSTGEO) ia = kxy ? inv.z : (kxz ? inv.y : inv.x);  // (= ia_hit)
+          const float tr = hit_plane_t(n_, da, ia, plane_t(n_, ia));  // the winner's t, corrected
           x = mk(keep(o.x + d.x * tr), keep(o.y + d.y * tr), keep(o.z + d.z * tr));
           // a miss vertex is the origin (:373-374); a leaked path ending at its miss (every LREF
           // kernel, see below) never reads it
           if constexpr (CF::LREF != 1) x = hit ? x : mk(0, 0, 0);
-          l_miss += hit ? 0u : 1u;
+          if constexpr (!kEarly) l_miss += hit ? 0u : 1u;
           const float sg = da < 0.0f ? 1.0f : -1.0f;
           nl = mk(kyz ? sg : 0.0f, kxz ? sg : 0.0f, kxy ? sg : 0.0f);
           if (TP::MAT) gn = mk(kyz ? 1.0f : 0.0f, kxz ? 1.0f : 0.0f, kxy ? 1.0f : 0.0f);
         } else {
         if (!hit) {
           x = mk(0, 0, 0);
-          ++l_miss;
+          if constexpr (!kEarly) ++l_miss;
         } else {
           // plane distance as the reference derives it (:103); spheres: the root
           float tr = hit_t<TP>(H, hpos, o, d, ia_hit, G);
@@ -1202,7 +1257,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         // unconditionally saves the register copies of a conditional update.
         T = mk(T.x * f.x, T.y * f.y, T.z * f.z);
         o = x;
-        vid = id;
+        if constexpr (!kEarlyNee) vid = id;
         uint32_t nxt = kStCos;  // the state after this vertex unless the path ends here
         if (TP::MAT && !term && H.refl != SPT_DIFF) {
           // SPEC :481-482 and REFR :484-495 (smallpt's commented-out code; oracle c_path): no NEE.
@@ -1311,7 +1366,7 @@ render_kernel(const KParams* __restrict__ Pg) {
             } else {
               la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
             }
-            const bool cand = (id == light_id_of<CF>(D)) | la;
+            const bool cand = (id == light_slot_of<TP, CF>(D)) | la;
             d = dl;  // a rejected lane generates its cosine direction next iteration anyway
             nxt = early ? kStEarly : (cand ? kStShadow : kStCos);
           }
@@ -1327,9 +1382,12 @@ render_kernel(const KParams* __restrict__ Pg) {
         if (traced_shadow || ls == kStEarly) {
           SPT_REGION(6);
           const bool ea = ls == kStEarly;
-          const bool lh = ea | (id == kRefLightId);
+          // a traced shadow ray that reached the light; never a proven lane (its path ray hit what
+          // it shaded, not the black light, which would have ended the path)
+          const bool th = id == light_slot_of<TP, CF>(cptr(Pg));
+          const bool lh = ea | th;
           if (lh) SPT_REGION(7);
-          l_hit += lh ? 1u : 0u;
+          count_if(l_hit, th);  // (+ the proven ones, l_early / s_nearly, at the end)
           if constexpr (TP::SPH) {  // (sphere kernels ballot-count the traced ones)
             if (ea) atomicAdd(&s_nearly[threadIdx.x / 64], 1u);
           } else {
@@ -1340,14 +1398,15 @@ render_kernel(const KParams* __restrict__ Pg) {
           // (k_L - o.y) / d.y as the trace ranked it (the light is an XZ rect in both kernels)
           float kl;
           if constexpr (kEarlyNee) kl = kCornellRects[kCornellLightPos].k;
-          else kl = s_prims[kRefLightId].w1;
-          const float tl = ea ? t : plane_t(kl - o.y, ia_hit);
+          else kl = s_prims[light_slot_of<TP, CF>(cptr(Pg))].w1;
+          // (the light is an XZ rect: its 1/d is the y axis')
+          const float tl = ea ? t : plane_t(kl - o.y, TP::CONSTGEO ? inv.y : ia_hit);
           // (computed for every resolving lane: a branch around it cost exec-mask SALU)
           const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
           // the black light ends a path that reaches it, so only the light vertex's L needs T*w
           // (a lane whose shadow ray is blocked keeps T: the cosine sample follows)
           const f3 Tw = mk(T.x * wl, T.y * wl, T.z * wl);
-          const DevPrim& H = s_prims[kRefLightId];
+          const DevPrim& H = s_prims[light_slot_of<TP, CF>(cptr(Pg))];
           const f3 Le = mk(fmaf(Tw.x, H.ex, L.x), fmaf(Tw.y, H.ey, L.y), fmaf(Tw.z, H.ez, L.z));
           L = mk(lh ? Le.x : L.x, lh ? Le.y : L.y, lh ? Le.z : L.z);
           ls = lh ? kStTerm : kStCos;
@@ -1461,6 +1520,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         atomicAdd(st + 2, (unsigned long long)l_nee);
         atomicAdd(st + 4, (unsigned long long)l_nee);
       }
+      if constexpr (kEarlyNee) l_hit += l_early;  // proven shadow rays reach the light
       atomicAdd(st + 3, (unsigned long long)l_hit);
       atomicAdd(st + 5, (unsigned long long)l_hit);
       atomicAdd(st + 7, (unsigned long long)l_miss);
@@ -1477,6 +1537,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           const unsigned long long ne = s_nearly[threadIdx.x / 64];
           atomicAdd(st + kStatShadowProven, ne);
           atomicAdd(st + kStatShadowTraced, ne);
+          atomicAdd(st + 3, ne);  // proven shadow rays reach the light (vertices, light hits)
+          atomicAdd(st + 5, ne);
         }
       }
     }
