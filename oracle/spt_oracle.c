@@ -501,8 +501,8 @@ float spt_oracle_rsq_nr(float x) {
   }
   return y;
 }
-/* The same reciprocal square root with two Newton steps (relative error < 5e-6): the free-scale
- * contract's normalize (c_unit_dirs), where a direction need only be unit to ~1e-5. */
+/* The same reciprocal square root with two Newton steps (relative error < 5e-6): the sphere root
+ * (c_sphere; rounds 1-4 also the free-scale contract's directions, now spt_oracle_rsq_nr1). */
 float spt_oracle_rsq_nr2(float x) {
   float y = asf(0x5F375A86u - (asu(x) >> 1));
   const float h = 0.5f * x;
@@ -513,9 +513,19 @@ float spt_oracle_rsq_nr2(float x) {
   }
   return y;
 }
-static inline fv fnormalize2(fv v) {
+/* Contract v7: the free-scale contract's direction rsqrt takes ONE Newton step (relative error
+ * < 1.8e-5, from below; rounds 1-4 took two). Measured on this oracle, 128x96 @ 16, 12 seeds, NEE:
+ * first misses +0.25 % (1 step in the normalize, 0.6 sigma), -0.04 % (1 step in the cosine
+ * sample's R); with the bare seed in the normalize (|d| = 1 within 3.4e-3) +2.3 % (5 sigma), so
+ * not that. */
+float spt_oracle_rsq_nr1(float x) {
+  const float y = asf(0x5F375A86u - (asu(x) >> 1));
+  const float hy = (0.5f * x) * y;
+  return y * fmaf(-hy, y, 1.5f);
+}
+static inline fv fnormalize_free(fv v) {
   const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
-  const float inv = spt_oracle_rsq_nr2(l2);
+  const float inv = spt_oracle_rsq_nr1(l2);
   return fv3(v.x * inv, v.y * inv, v.z * inv);
 }
 /* Vec::norm :50-52 as v * rsq_nr(len2). (Round 1 returned exactly-unit vectors unchanged, as the
@@ -649,8 +659,9 @@ typedef struct {
  * something needs |d| = 1 to fp32 accuracy: the sphere quadratic (:229-239 assumes |d| = 1) and
  * the REFR Fresnel terms (:485-491 treat d.nl as a cosine). Otherwise (rectangles, DIFF/SPEC) the
  * FREE-SCALE contract:
- *  - path directions (camera ray, cosine sample) are normalised with two Newton steps
- *    (rsq_nr2, |d| = 1 within 5e-6). They must stay unit to ~1e-4: the self-hit / leak rate of the
+ *  - path directions (camera ray, cosine sample) are normalised with one Newton step
+ *    (rsq_nr1, |d| = 1 within 2e-5; contract v7, rounds 1-4: two). They must stay unit to ~1e-4:
+ *    the self-hit / leak rate of the
  *    rect tests depends on |d| (measured, 256x192 @ 64 cosine-only: misses per sample 0.458 at
  *    |d| = 1 +- 1e-3, but 0.67 at |d| = 0.75 or 1.5 and 0.71 at 1.25), as on the reference's fp64
  *    unit vectors;
@@ -1186,14 +1197,14 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform, int unit) {
   spt_oracle_disk_dir(ra, &c, &s); /* the azimuth r1 = 2*pi*xi1 of :343 */
   if (uniform) {
     const float m = xi2 * (2.0f - xi2);
-    r2s = m * (unit ? spt_oracle_rsq_nr(m) : spt_oracle_rsq_nr2(m));
+    r2s = m * (unit ? spt_oracle_rsq_nr(m) : spt_oracle_rsq_nr1(m));
     s1 = 1.0f - xi2;
   } else {
     /* (cos, sin) * sqrt(r2) and sqrt(1 - r2) (:343-347) scaled by 1 / sqrt(1 - r2): the direction
        is normalized below anyway, so the contract takes R = sqrt(r2 / (1 - r2)) with ONE rsqrt,
        R = r2 * rsq(r2 * (1 - r2)), and a normal component of exactly 1. */
     const float q = xi2 * (1.0f - xi2);
-    r2s = xi2 * (unit ? spt_oracle_rsq_nr(q) : spt_oracle_rsq_nr2(q));
+    r2s = xi2 * (unit ? spt_oracle_rsq_nr(q) : spt_oracle_rsq_nr1(q));
     s1 = 1.0f;
   }
   cr = c * r2s;
@@ -1210,7 +1221,7 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform, int unit) {
     if (nl.x != 0.0f) r = fv3(nl.x * s1, sr, -(nl.x * cr));
     else if (nl.y != 0.0f) r = fv3(sr, nl.y * s1, nl.y * cr);
     else r = fv3(sr, -(nl.z * cr), nl.z * s1);
-    return unit ? fnormalize(r) : fnormalize2(r);
+    return unit ? fnormalize(r) : fnormalize_free(r);
   }
   a = fabsf(nl.x) > 0.1f ? fv3(nl.z, 0.0f, -nl.x) : fv3(0.0f, -nl.z, nl.y);
   u = fnormalize(a);
@@ -1218,7 +1229,7 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform, int unit) {
   {
     const fv r = fv3(fmaf(nl.x, s1, fmaf(v.x, sr, u.x * cr)), fmaf(nl.y, s1, fmaf(v.y, sr, u.y * cr)),
                      fmaf(nl.z, s1, fmaf(v.z, sr, u.z * cr)));
-    return unit ? fnormalize(r) : fnormalize2(r);
+    return unit ? fnormalize(r) : fnormalize_free(r);
   }
 }
 
@@ -1314,7 +1325,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
     }
     o = fv3(cam[0], cam[1], cam[2]);
     d = fv3(v[0], v[1], v[2]);
-    d = C->unit ? fnormalize(d) : fnormalize2(d);
+    d = C->unit ? fnormalize(d) : fnormalize_free(d);
   }
   st->samples++;
   for (;;) {

@@ -235,7 +235,7 @@ struct Topo {
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
   static constexpr bool WIDE = WIDE_;  // fp64 wide spheres may occur (their own kernel: VGPRs)
   // Ray-direction contract (oracle c_unit_dirs): 1 = unit directions (spheres, REFR), 0 = free-scale
-  // (rect-only DIFF scenes: path directions normalised with rsq_nr2, the NEE vector not at all),
+  // (rect-only DIFF scenes: path directions normalised with rsq_nr1, the NEE vector not at all),
   // -1 = KParams::unit_dirs at run time (the generic kernels)
   static constexpr int DIRS = MAT_ ? -1 : (SPH_ ? 1 : 0);
 };
@@ -879,7 +879,9 @@ render_kernel(const KParams* __restrict__ Pg) {
   int sp = 0;             // pending refraction children in s_stack (MAT only)
   uint32_t lp = 0, s = 0, s_end = 0;
   PxKey pk = PxKey{0, 0, 0};  // Philox round-1/2 terms of the unit's pixel (philox_pixel_key)
-  int depth = 0, vid = 0;  // depth: vertices of the current path so far (0 until its first)
+  // dp1: vertices of the current path so far plus one (1 until its first) -- the Philox vertex
+  // counter of the ray generated next, with no add per call
+  int dp1 = 1, vid = 0;
   // camera raster terms of the unit's pixel, fx = (x - 0.5) - 128, fy = (h - y - 1 - 0.5) - 128;
   // the axis-aligned camera kernels hold P_x, P_y (jitter_f) here instead
   float fx = 0.0f, fy = 0.0f;
@@ -1077,8 +1079,8 @@ render_kernel(const KParams* __restrict__ Pg) {
       if (ls != kStSpec) SPT_REGION(cam ? 3 : 8);
       const bool unit = unit_dirs_of<TP>(Pg);
       f3 v = cosine_vec<!TP::SPH>(nl, r.z, r.w, TP::MAT && cptr(Pg)->scatter_uniform != 0, unit);
-      // the vertex this ray leads to: depth + 1 (depth == 0 for a new sample's camera ray)
-      const uint32_t ctr2 = ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u);
+      // the vertex this ray leads to: dp1 (1 for a new sample's camera ray)
+      const uint32_t ctr2 = (uint32_t)dp1 | (TP::MAT ? branch << 24 : 0u);
       r = philox_px(pk, s, ctr2);
       {
         const SPT_CONST KParams* C = cptr(Pg);
@@ -1099,7 +1101,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         }
         v = mk(cam ? vc.x : v.x, cam ? vc.y : v.y, cam ? vc.z : v.z);  // o: set at the path end
       }
-      const f3 dn = normalize_dir(v, unit);  // rsq_nr2 in the free-scale contract
+      const f3 dn = normalize_dir(v, unit);  // rsq_nr1 in the free-scale contract (v7)
       if constexpr (TP::MAT) {  // a SPEC/REFR direction is set already
         const bool kd = ls == kStSpec;
         d = mk(kd ? d.x : dn.x, kd ? d.y : dn.y, kd ? d.z : dn.z);
@@ -1157,7 +1159,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         // A black light (HEAD :294) ends the path there by RR with p == 0 (:448-453) without a
         // random draw; anything else is shaded with that vertex's own Philox words.
         if (CF::BLACK != 1 && lh && !(hit && s_prims[id].pmax == 0.0f))
-          r = philox_px(pk, s, ((uint32_t)depth + 1u) | (TP::MAT ? branch << 24 : 0u));
+          r = philox_px(pk, s, (uint32_t)dp1 | (TP::MAT ? branch << 24 : 0u));
         ls = lh ? kStPath : kStCos;
       }
 
@@ -1230,7 +1232,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         f3 f = mk(H.cx, H.cy, H.cz);
         const f3 e = mk(H.ex, H.ey, H.ez);
         const int rr_t = H.rr_t;
-        ++depth;
+        const int depth = dp1++;  // this vertex's depth (1 = the first)
         u4 rl = r;  // RR / NEE-mix draws; at vertex 1 from stream 1 (only configs that need them)
         if (CF::NOS1 != 1 && depth == 1) {
           const SPT_CONST KParams* C = cptr(Pg);
@@ -1420,7 +1422,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           o = mk(N.o[0], N.o[1], N.o[2]);
           d = mk(N.d[0], N.d[1], N.d[2]);
           T = mk(N.T[0], N.T[1], N.T[2]);
-          depth = N.depth;
+          dp1 = N.depth + 1;
           branch = N.branch;
           ls = kStSpec;
         } else {
@@ -1432,7 +1434,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           ++s;
           L = mk(0, 0, 0);
           T = mk(1, 1, 1);
-          depth = 0;
+          dp1 = 1;
           {
             const SPT_CONST KParams* C = cptr(Pg);
             o = CF::CAMAX == 1 ? mk(ck.o0, ck.o1, ck.o2) : mk(C->cam[0], C->cam[1], C->cam[2]);
