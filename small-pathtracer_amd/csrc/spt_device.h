@@ -125,15 +125,16 @@ __device__ __forceinline__ float rsq_nr(float x) {
   return y;
 }
 
-// The same with one Newton step (relative error < 1.8e-5, always below the root): the free-scale
-// contract's directions (contract v7, oracle c_unit_dirs), where a path direction need only be unit
-// to ~1e-4 and the cosine sample's tangent scale R may be off by 2e-5.
+// The same with one Newton step (relative error < 1.8e-3, always below the root): the free-scale
+// contract's normalize of the path directions (contract v7, oracle c_unit_dirs). Not the cosine
+// sample's R, whose error would bias the sampled distribution.
 __device__ __forceinline__ float rsq_nr1(float x) {
   const float y = __uint_as_float(0x5F375A86u - (__float_as_uint(x) >> 1));
   const float hy = (0.5f * x) * y;
   return y * fmaf(-hy, y, 1.5f);
 }
-// With two Newton steps (relative error < 5e-6): the sphere root (oracle c_sphere).
+// With two Newton steps (relative error < 5e-6): the cosine sample's R in the free-scale contract
+// and the sphere root (oracle c_sphere).
 __device__ __forceinline__ float rsq_nr2(float x) {
   float y = __uint_as_float(0x5F375A86u - (__float_as_uint(x) >> 1));
   const float h = 0.5f * x;
@@ -164,7 +165,9 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
   return mk(v.x * inv, v.y * inv, v.z * inv);
 }
 // The free-scale contract's normalize (contract v7, oracle fnormalize_free): rsq with ONE Newton
-// step, |d| = 1 within 2e-5 (rounds 1-4: two steps, 5e-6; C3 -1 %, leak statistics unchanged).
+// step, |d| = 1 within 1.8e-3 (rounds 1-4: two steps, 5e-6). The scale of a path direction places
+// no geometry -- the hit point o + d t is the same real point -- it only moves the roundings that
+// set the self-hit / leak statistics, which stay within 0.3 %.
 __device__ __forceinline__ f3 normalize3_free(f3 v) {
   const float l2 = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
   const float inv = rsq_nr1(l2);
@@ -227,7 +230,7 @@ __device__ __forceinline__ void disk_dir(uint32_t ra, float& c_out, float& s_out
 // axis-aligned (rect-only scenes); otherwise it is tested per lane, as the oracle does.
 // uniform: the reference's commented-out uniform hemisphere (:352-359), radial sqrt(r2(2-r2)) and
 // normal component 1-r2 (SPT_FLAG_UNIFORM_SCATTER; oracle c_cosine).
-// unit: the unit-direction contract (rsq_nr) or the free-scale one (rsq_nr1; oracle c_unit_dirs).
+// unit: the unit-direction contract (rsq_nr) or the free-scale one (rsq_nr2; oracle c_unit_dirs).
 template <bool AXIS = false>
 __device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool uniform, bool unit) {
   const float xi2 = u01(rb);
@@ -236,14 +239,14 @@ __device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool u
   float r2s, s1;
   if (uniform) {
     const float m = xi2 * (2.0f - xi2);
-    r2s = m * (unit ? rsq_nr(m) : rsq_nr1(m));
+    r2s = m * (unit ? rsq_nr(m) : rsq_nr2(m));
     s1 = 1.0f - xi2;
   } else {
     // Contract (oracle c_cosine): sqrt(r2) and sqrt(1 - r2) of :343-347 scaled by 1/sqrt(1 - r2),
     // since the kernel normalizes the direction anyway: R = sqrt(r2 / (1 - r2)) with ONE rsqrt,
     // R = r2 * rsq(r2 * (1 - r2)) (r2 = 0 gives 0), and a normal component of exactly 1.
     const float q = xi2 * (1.0f - xi2);
-    r2s = xi2 * (unit ? rsq_nr(q) : rsq_nr1(q));
+    r2s = xi2 * (unit ? rsq_nr(q) : rsq_nr2(q));
     s1 = 1.0f;
   }
   const float cr = c * r2s, sr = s * r2s;
