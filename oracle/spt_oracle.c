@@ -1031,7 +1031,9 @@ static int c_early_nee_proven(fv o, fv d, float* tl) {
   const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && c_key(tt, 8) < C_KEY_NONE;
   const int room = asu(o.x) - asu(1.0f) <= asu(99.0f) - asu(1.0f) && asu(o.z) <= asu(170.0f) &&
                    asu(o.y) < asu(81.5f);
-  const int short_box = o.y >= 25.0f || (o.x <= 63.0f && a < 13.0f);
+  /* (round 4: "x_L < 63", a < 13, dropped as in the kernel: below y = 25 the reference's light
+     samples, x in [31, 33), cross y = 81.5 at x_L < 33.2; the proof tests check the claims) */
+  const int short_box = o.y >= 25.0f || o.x <= 63.0f;
   const int tall_box = o.y >= 50.0f || o.z >= 62.0f;
   *tl = tt;
   if (g_proof_on == 2) return acc && room && o.y > g_proof_y0; /* spt_kernel.hip early_room_proven */

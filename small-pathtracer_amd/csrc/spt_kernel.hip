@@ -705,7 +705,8 @@ __device__ __forceinline__ bool light_accepts(const SPT_CONST KParams* P, const 
 //     32..68), >= 63 in z (z 63..96); the ceiling is 0.1 above the light plane.
 //   * short box (x, z in [63, 88], y <= 25): y >= 25 (the ray rises: the slab's y interval ends at
 //     t <= 0, so the box's candidate is negative), or x <= 63 and x_L < 63 (x stays below 63 along
-//     the segment but at its start; a vertex exactly on the x = 63 face has t = -2^-149 there).
+//     the segment but at its start; a vertex exactly on the x = 63 face has t = -2^-149 there;
+//     x_L < 63 always holds below y = 25, see early_nee_proven).
 //   * tall box (x in [12, 42], z in [32, 62], y <= 50): y >= 50, or z >= 62 (z stays at or above 62
 //     along the segment -- the light's z >= 63 -- and reaches 62 only at t <= 0: the box's z slab
 //     ends behind the origin). Round 4: >= and <= where rounds 2-3 kept a 0.01 margin; a vertex on
@@ -726,9 +727,12 @@ __device__ __forceinline__ int early_room_ok(f3 x) {
 __device__ __forceinline__ bool early_room_proven(f3 x, float y0) {
   return (early_room_ok(x) & (int)(x.y > y0)) != 0;
 }
-__device__ __forceinline__ bool early_nee_proven(f3 x, float a_light) {
+// (Round 4: the short box's "x_L < 63" is implied below y = 25: the reference's wrapped light
+// samples lie at x in [31, 33), and the crossing of y = 81.5 lies within 0.1 / (81.6 - y) < 0.0018
+// of the way back to the vertex, so x_L < 33.2 there. One compare fewer; the same predicate.)
+__device__ __forceinline__ bool early_nee_proven(f3 x) {
   const int room = early_room_ok(x);
-  const int short_box = (int)(x.y >= 25.0f) | ((int)(x.x <= 63.0f) & (int)(a_light < 13.0f));
+  const int short_box = (int)(x.y >= 25.0f) | (int)(x.x <= 63.0f);
   const int tall_box = (int)(x.y >= 50.0f) | (int)(x.z >= 62.0f);
   return (room & short_box & tall_box) != 0;
 }
@@ -889,6 +893,7 @@ render_kernel(const KParams* __restrict__ Pg) {
   // o starts at the camera (the first ray of every sample is a camera ray; the path end resets it)
   f3 o = mk(cptr(Pg)->cam[0], cptr(Pg)->cam[1], cptr(Pg)->cam[2]);
   f3 d = mk(0, 0, 1), T = mk(1, 1, 1), L = mk(0, 0, 0), nl = mk(0, 1, 0);
+  float w_nee = 0.0f;  // HEAD NEE kernel: the NEE weight of the lane's shadow ray, from its vertex
   u4 r = u4{0, 0, 0, 0};  // Philox words of the vertex the pending path ray leads to
   // ---- wave-uniform state
   // Camera and fixed-point constants of the axis-aligned camera kernels, loaded once and held in
@@ -1170,6 +1175,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         const int kind = H.kind;
         f3 x;
         f3 gn = mk(0, 0, 0);
+        bool ax_xy = false, ax_xz = false;  // the normal's axis (rect-only kernels)
         if constexpr (!TP::SPH) {
           // Rect-only scenes, branch-free: the plane axis of the hit kind selects (o_a, d_a); the
           // hit point re-derives t = (k - o_a) / d_a as the reference does (:103) and
@@ -1182,6 +1188,8 @@ render_kernel(const KParams* __restrict__ Pg) {
             kxy = kind == SPT_RECT_XY;
             kxz = kind == SPT_RECT_XZ;
           }
+          ax_xy = kxy;
+          ax_xz = kxz;
           const bool kyz = !kxy && !kxz;
           const float oa = kxy ? o.z : (kxz ? o.y : o.x);
           const float da = kxy ? d.z : (kxz ? d.y : d.x);
@@ -1357,8 +1365,15 @@ render_kernel(const KParams* __restrict__ Pg) {
               const RectHit h = rect_eval(CornellRectPtr{kCornellLightPos},
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
               la = h.inb & key_valid(h.tt, kCornellLightPos);
-              early = la & early_nee_proven(x, h.a);
-              t = early ? h.tt : t;  // the t the trace would return (the light's test, same bits)
+              early = la & early_nee_proven(x);
+              // The weight of :471-472 now, for a proven lane and a traced one alike: nee_weight's
+              // arithmetic with |dl . nl| = |dl_a| on the normal's axis a (the dot's zero terms are
+              // exact) and t = the light's own t, the bits the trace returns for it. The resolve
+              // then needs neither the light's t nor the weight (round 4: -5 VALU per iteration).
+              const float adot = fabsf(ax_xy ? dl.z : (ax_xz ? dl.y : dl.x));
+              const float num = fabsf(dl.y) * adot;
+              const float vv = dot3(dl, dl);
+              w_nee = (num * kRefNeeC) * rcp_nr((h.tt * h.tt) * (vv * vv));
             } else if constexpr (kEarlySph) {  // the uploaded light rect (XZ, host-checked)
               const RectHit h = rect_eval(G2->rect + D->light_pos,
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
@@ -1396,15 +1411,17 @@ render_kernel(const KParams* __restrict__ Pg) {
             l_early += ea ? 1u : 0u;
             ++l_shadow;
           }
-          // the light's t: the pre-test's for a proven lane, else the traced light hit's own
-          // (k_L - o.y) / d.y as the trace ranked it (the light is an XZ rect in both kernels)
-          float kl;
-          if constexpr (kEarlyNee) kl = kCornellRects[kCornellLightPos].k;
-          else kl = s_prims[light_slot_of<TP, CF>(cptr(Pg))].w1;
-          // (the light is an XZ rect: its 1/d is the y axis')
-          const float tl = ea ? t : plane_t(kl - o.y, TP::CONSTGEO ? inv.y : ia_hit);
-          // (computed for every resolving lane: a branch around it cost exec-mask SALU)
-          const float wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
+          float wl;
+          if constexpr (kEarlyNee) {
+            wl = w_nee;  // (from the vertex, above)
+          } else {
+            // the light's t: the pre-test's for a proven lane, else the traced light hit's own
+            // (k_L - o.y) / d.y as the trace ranked it (the light is an XZ rect)
+            const float kl = s_prims[light_slot_of<TP, CF>(cptr(Pg))].w1;
+            const float tl = ea ? t : plane_t(kl - o.y, ia_hit);
+            // (computed for every resolving lane: a branch around it cost exec-mask SALU)
+            wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
+          }
           // the black light ends a path that reaches it, so only the light vertex's L needs T*w
           // (a lane whose shadow ray is blocked keeps T: the cosine sample follows)
           const f3 Tw = mk(T.x * wl, T.y * wl, T.z * wl);
