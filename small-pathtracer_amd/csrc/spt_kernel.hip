@@ -1423,11 +1423,13 @@ render_kernel(const KParams* __restrict__ Pg) {
             wl = keep(nee_weight(unit_dirs_of<TP>(Pg), d, nl, tl, kRefLarea, kRefNeeC));
           }
           // the black light ends a path that reaches it, so only the light vertex's L needs T*w
-          // (a lane whose shadow ray is blocked keeps T: the cosine sample follows)
-          const f3 Tw = mk(T.x * wl, T.y * wl, T.z * wl);
+          // (a lane whose shadow ray is blocked keeps T: the cosine sample follows). A blocked
+          // lane adds (T*0)*e = +0 instead of selecting: L + 0 is L bit for bit, T being finite
+          // and >= 0 on a path that has not reached the light (one select, not three)
+          const float wh = lh ? wl : 0.0f;
+          const f3 Tw = mk(T.x * wh, T.y * wh, T.z * wh);
           const DevPrim& H = s_prims[light_slot_of<TP, CF>(cptr(Pg))];
-          const f3 Le = mk(fmaf(Tw.x, H.ex, L.x), fmaf(Tw.y, H.ey, L.y), fmaf(Tw.z, H.ez, L.z));
-          L = mk(lh ? Le.x : L.x, lh ? Le.y : L.y, lh ? Le.z : L.z);
+          L = mk(fmaf(Tw.x, H.ex, L.x), fmaf(Tw.y, H.ey, L.y), fmaf(Tw.z, H.ez, L.z));
           ls = lh ? kStTerm : kStCos;
         }
       }
