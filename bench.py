@@ -256,6 +256,70 @@ def image_writer(spt, full, w, h, with_cpu: bool):
     return out
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, timeout_s: float, env=None) -> int:
+    """`bench.py --gpus N` without a launcher: start N copies of this script as child processes,
+    one rank per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR = 127.0.0.1, a free
+    MASTER_PORT), and wait for them. The parent never touches the GPU (no torch import, no HIP
+    call): it only starts processes, so nothing is exec'd from a process that initialised the GPU.
+    The children inherit stdout, so rank 0's JSON line is the parent's output (the other ranks print
+    none). Returns 0 when every rank exits 0. Otherwise it returns the first failing rank's status
+    (124 when the ranks outlive `timeout_s`), after ending the remaining children: each runs in its
+    own process group, and the parent kills exactly those groups. No retry.
+    The reference's own parallel construct is an OpenMP pragma over rows (smallpt.cpp:526-528)."""
+    import signal
+    import subprocess
+
+    base = dict(os.environ if env is None else env)
+    base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(free_port()), SPT_BENCH_SPAWNED="1")
+    procs = []
+    for i in range(n):
+        e = dict(base, RANK=str(i), LOCAL_RANK=str(i))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=e, start_new_session=True))
+    deadline = time.monotonic() + timeout_s
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc  # -N (signal N) -> 128 + N
+                log(f"bench.py: rank {procs.index(p)} exited with status {rc}; ending the other ranks")
+        if status != 0 or time.monotonic() > deadline:
+            if status == 0:
+                status = 124
+                log(f"bench.py: ranks still running after {timeout_s:.0f} s; ending them (status 124)")
+            for p in live:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+            for p in live:
+                try:
+                    p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                    p.wait()
+            break
+        time.sleep(0.05)
+    return status
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -273,6 +337,9 @@ def main() -> None:
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--kernel-level", default="auto", help="A/B only: cap the kernel specialisation "
                     "(auto | generic | cornell | const; spt_params.flags, never changes results)")
+    ap.add_argument("--reference-leaks", action="store_true",
+                    help="leaked paths go on from the miss vertex as the reference's (:371-377; "
+                         "SPT_FLAG_REFERENCE_LEAKS) instead of ending at their first miss (contract v6)")
     ap.add_argument("--verify-gather", dest="verify_gather", action="store_true", default=None,
                     help="rank 0 re-renders the whole image alone and checks the gathered one bit for "
                          "bit (default on for N > 1: the RCCL gather has not run on hardware before)")
@@ -287,7 +354,25 @@ def main() -> None:
     ap.add_argument("--init-timeout", type=float, default=300.0,
                     help="seconds allowed for the RCCL / process-group set-up; past it the rank "
                          "prints an error and exits with status 3 (no retry)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N > 1 without a launcher: seconds the spawned ranks may run in all "
+                         "before they are ended (exit status 124)")
+    ap.add_argument("--probe-env", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun: start the N ranks here, before anything loads HIP (launch_ranks)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
+    if args.probe_env:
+        # CPU test hook (tests/test_bench_launch.py): report the rank environment, no GPU work
+        rk = os.environ.get("RANK", "0")
+        print(json.dumps({k: os.environ.get(k) for k in
+                          ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                           "SPT_BENCH_SPAWNED")}), flush=True)
+        if os.environ.get("SPT_PROBE_HANG_RANK") == rk:
+            time.sleep(3600)
+        sys.exit(int(os.environ.get("SPT_PROBE_EXIT", "0")) if
+                 os.environ.get("SPT_PROBE_FAIL_RANK") == rk else 0)
 
     import datetime
     import threading
@@ -335,10 +420,11 @@ def main() -> None:
     prims = spt.cornell_scene() if cfg["scene"] == "cornell" else spt.spheres32_scene()
     w, h = cfg["width"], cfg["height"]
     cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    leak_flag = spt.FLAG_REFERENCE_LEAKS if args.reference_leaks else 0
     params = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
                                 max_depth=cfg["max_depth"], tile_rows=8, shard_index=rank,
                                 shard_count=world, device=local, chunk=args.chunk,
-                                flags=spt.kernel_flag(args.kernel_level))
+                                flags=spt.kernel_flag(args.kernel_level) | leak_flag)
     rows_of = sd.shard_row_lists(h, 8, world)
     my_rows = rows_of[rank]
     assert np.array_equal(spt.shard_rows(params), my_rows)
@@ -484,16 +570,51 @@ def main() -> None:
         rens[0].render_async(prims, cam, params, shards[0].data_ptr(), streams[0].cuda_stream)
         iso.append(rens[0].stats())
     torch.cuda.synchronize()
+    kst = iso if iso else kstats
+    kms = np.array([s["kernel_ms"] for s in kst])
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cuda" if backend == "nccl" else "cpu")
+        # Per-rank evidence for the N > 1 line: each rank's isolated kernel time, its timed-region
+        # wall time and the gather alone (3 gathers after a barrier each, the fastest; the image
+        # they gather is the frame just rendered into buffer 0, so nothing checked changes).
+        gms = []
+        for _ in range(3):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t_ = time.perf_counter()
+            if comm is not None:
+                comm.gather(params, shards[0].data_ptr(), fulls[0].data_ptr() if rank == 0 else 0,
+                            streams[0].cuda_stream)
+            elif use_torch_gather:
+                sd.gather_rows(shards[0], rows_of, fulls[0], gather_list=slots)
+            else:
+                host = sd.gather_rows(shards[0].cpu(), rows_of, fulls[0].cpu() if rank == 0 else None)
+                if rank == 0:
+                    fulls[0].copy_(host)
+            torch.cuda.synchronize()
+            gms.append((time.perf_counter() - t_) * 1e3)
+        dev = "cuda" if backend == "nccl" else "cpu"
+        mine = torch.tensor([float(kms.mean()), kms_flight, elapsed * 1e3, min(gms)],
+                            dtype=torch.float64, device=dev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        every = np.stack([e.cpu().numpy() for e in every])
+        per_rank = {"kernel_ms": [round(float(x), 3) for x in every[:, 0]],
+                    "kernel_ms_min": round(float(every[:, 0].min()), 3),
+                    "kernel_ms_max": round(float(every[:, 0].max()), 3),
+                    "kernel_ms_in_flight": [round(float(x), 3) for x in every[:, 1]],
+                    "timed_region_ms": [round(float(x), 2) for x in every[:, 2]],
+                    "gather_ms": [round(float(x), 3) for x in every[:, 3]],
+                    "gather_ms_source": "3 gathers alone after the timed region, each after a "
+                                        "barrier, fastest (wall clock incl. the barrier release)",
+                    "launcher": ("bench.py (spawned ranks)" if os.environ.get("SPT_BENCH_SPAWNED")
+                                 else "external (torch.distributed.run or equivalent)")}
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     samples_per_step = w * h * spp  # all ranks together (each rank renders its rows at spp)
     value = samples_per_step * args.steps / elapsed / 1e6
-    kst = iso if iso else kstats
-    kms = np.array([s["kernel_ms"] for s in kst])
     flop = np.array([s["flop"] for s in kst])
     flop_x = np.array([s["flop_executed"] for s in kst])
     achieved = float((flop / (kms * 1e-3)).mean() / 1e12)
@@ -543,7 +664,8 @@ def main() -> None:
         img = full.cpu().numpy()
         if args.verify_gather:  # the whole image on this GPU alone (1 shard) must equal the gather
             p1 = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
-                                    max_depth=cfg["max_depth"], tile_rows=8, device=local)
+                                    max_depth=cfg["max_depth"], tile_rows=8, device=local,
+                                    flags=leak_flag)
             one = spt.render(prims, cam, p1)
             gather_exact = bool(np.array_equal(one, img))
             assert gather_exact, "gathered image differs from the 1-GPU render"
@@ -567,7 +689,7 @@ def main() -> None:
             # 15 more seeds of the same render (after the timed region): the matched-budget RMSE
             extra = [spt.render(prims, cam, spt.default_params(
                 width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"], max_depth=cfg["max_depth"],
-                tile_rows=8, device=local, seed=sd_)) for sd_ in range(2, 17)]
+                tile_rows=8, device=local, seed=sd_, flags=leak_flag)) for sd_ in range(2, 17)]
             qual = quality(img, spp, extra)
         if qual is not None and port is not None:
             # the bench's own rows re-rendered by the CPU contract (cpu_baseline.port): exact
@@ -631,6 +753,7 @@ def main() -> None:
             "quality": qual,
             "gather_equals_1gpu_render": gather_exact,
             "gather": gather_mode,
+            "ranks": per_rank,
             "cpu_baseline": cpu,
             "image_writer": writer,
         }

@@ -25,9 +25,9 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 4 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed;
+#define SPT_ABI_VERSION 5 /* 2: spt_stats gained shadow_traced, sphere_vertices, flop_executed;
                              3: shadow_proven; 4: spt_gather_plan, spt_deinterleave_source,
-                             spt_gather_staging_floats, spt_shutdown */
+                             spt_gather_staging_floats, spt_shutdown; 5: SPT_FLAG_REFERENCE_LEAKS */
 
 typedef enum spt_status {
   SPT_OK = 0,
@@ -103,6 +103,13 @@ typedef struct spt_params {
  * dir = u cos(r1) sqrt(r2(2-r2)) + v sin(r1) sqrt(r2(2-r2)) + w (1-r2)) instead of the live
  * cosine-weighted code (:340-347); the estimator weight stays 1, as in the reference. */
 #define SPT_FLAG_UNIFORM_SCATTER 1u
+/* Leaked paths (a path ray that misses every primitive, :371-377) go on from the miss vertex --
+ * the origin, with prim 0's material -- exactly as the reference's do. Without this flag the
+ * contract's leak-end rule applies wherever the host can prove it (contract v6: the
+ * scene has a closed room, the origin lies outside it, prim 0 does not emit and every emitter lies
+ * inside): such a path ends at its first miss, which skips the reference's post-leak vertices (~4 %
+ * of them in the HEAD scene) and changes the image's mean by ~8 ppm. */
+#define SPT_FLAG_REFERENCE_LEAKS 4u
 /* Kernel specialisation cap, flags bits 8-9 (A/B comparisons and tests; never changes a result:
  * every kernel computes the same contract bit for bit). AUTO (0) runs the most specialised kernel
  * the host can prove applicable to the scene and params; the others stop at that level. */

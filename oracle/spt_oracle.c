@@ -853,7 +853,8 @@ static void c_find_boxes(c_ctx* C, const spt_prim* s) {
  * leak's own mechanism in reverse) and its NEE ray then reaches the light: measured, 8 ppm of the
  * image's mean at 256x192 @ 64 (207 of 49 152 pixels differ by one sample each; cosine-only: none),
  * for 4 % fewer vertices -- the reference's post-leak wandering (tests/test_oracle.py, P2
- * re-checked). spt_oracle_set_leak_end(0) restores the reference's behaviour; statistics count
+ * re-checked). spt_params.flags SPT_FLAG_REFERENCE_LEAKS (and the test hook
+ * spt_oracle_set_leak_end(0)) restores the reference's behaviour; with the rule on, statistics count
  * first misses. */
 static int g_leak_end = 1;
 void spt_oracle_set_leak_end(int on) { g_leak_end = on != 0; }
@@ -861,7 +862,7 @@ static void c_find_leak_end(c_ctx* C, const spt_prim* s) {
   double lo[3], hi[3]; /* room box per axis x, y, z from the room pairs' planes (doubles) */
   int i, a;
   C->leak_end = 0;
-  if (!g_leak_end || C->room[0] < 0) return;
+  if (!g_leak_end || (C->P->flags & SPT_FLAG_REFERENCE_LEAKS) || C->room[0] < 0) return;
   for (a = 0; a < 3; a++) { /* room[0] XY pair: planes z; room[1] XZ: y; room[2] YZ: x */
     const c_test* T = &C->tests[C->room[a]];
     const double k0 = s[T->id0].geom[4], k1 = s[T->id1].geom[4];

@@ -108,6 +108,9 @@ EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_sc
            "spt_gather_plan", "spt_gather_staging_floats", "spt_deinterleave_source"]
 IMAGE_FORMATS = {"p3": 0, "p6": 1, "pfm": 2}
 FLAG_UNIFORM_SCATTER = 1  # spt_params.flags: random_scattering from the uniform code of :352-359
+# spt_params.flags: leaked paths go on from the miss vertex as the reference's (:371-377) instead of
+# ending at their first miss (contract v6's leak-end rule, the default where it applies)
+FLAG_REFERENCE_LEAKS = 4
 # spt_params.flags bits 8-9: cap on the kernel specialisation (A/B and tests; never changes results).
 # "head"/"auto": the most specialised kernel the host can prove applicable.
 KERNEL_LEVELS = {"auto": 0, "head": 0, "generic": 1, "cornell": 2, "const": 3}

@@ -1,8 +1,10 @@
 // smallpt_main.cpp — the reference's main() (smallpt.cpp:502-557) on the MI355X:
-//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--uniform] [--q Q]
+//   smallpt_amd [W H SPP [SEED [OUT.ppm]]] [--cos] [--uniform] [--reference-leaks] [--q Q]
 //               [--specular | --classic | --mirror-glass | --spheres32 [--max-depth D]]
 //               [--device N | --devices N] [--p6 | --pfm]
 //   --uniform: random_scattering from the commented-out uniform hemisphere code (:352-359)
+//   --reference-leaks: leaked paths go on from the miss vertex as the reference's (:371-377)
+//                      instead of ending at their first miss (SPT_FLAG_REFERENCE_LEAKS)
 //   --q Q: the NEE-mix probability of :464 (`q < Q`; 1 = HEAD, 0 = --cos)
 //   --specular: smallpt's mirror and glass balls (SPEC/REFR, :481-495) in the HEAD room
 //   --classic: the classic smallpt sphere box of the shipped image*.ppm (pure path tracing)
@@ -26,12 +28,13 @@ int main(int argc, char* argv[]) {
   int pos[4] = {512, 512, 16, 1};  // :507-508 defaults, seed 1
   const char* out = "image.ppm";
   bool cosine = false, uniform = false, specular = false, classic = false, mirror_glass = false;
-  bool spheres = false;
+  bool spheres = false, ref_leaks = false;
   int device = 0, devices = 0, max_depth = 0, npos = 0, format = SPT_IMAGE_P3, repeat = 1;
   float q = -1.0f;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--cos")) cosine = true;
     else if (!std::strcmp(argv[i], "--uniform")) uniform = true;
+    else if (!std::strcmp(argv[i], "--reference-leaks")) ref_leaks = true;
     else if (!std::strcmp(argv[i], "--specular")) specular = true;
     else if (!std::strcmp(argv[i], "--classic")) classic = true;
     else if (!std::strcmp(argv[i], "--mirror-glass")) mirror_glass = true;
@@ -54,6 +57,7 @@ int main(int argc, char* argv[]) {
   p.nee_prob = q >= 0.0f ? q : (cosine || box ? 0.0f : 1.0f);  // :464 (the sphere box: emission only)
   p.max_depth = max_depth;
   if (uniform) p.flags |= SPT_FLAG_UNIFORM_SCATTER;
+  if (ref_leaks) p.flags |= SPT_FLAG_REFERENCE_LEAKS;
   p.device = device;
   Camera cam(LOOKFROM, Vec(50, 40, 5), Vec(0, 1, 0), 65, float(p.width) / float(p.height));  // :521
   spt_stats st{};

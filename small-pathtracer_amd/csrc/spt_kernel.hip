@@ -199,8 +199,16 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
   unsigned long long* accum;  // [n_local_pix][3] 1.31 fixed point (stolen ranges; every unit without slots)
   unsigned long long* slots;  // [n_units][3] one owner store per unit, unit order (SPT_UNIT_SLOTS)
-  uint32_t* queue;            // [0] = next unit
+  // [0] = next unit (main launch), [16] = next leftover record (leftover launch), [32] = leftover
+  // records written (each on its own 64-byte line)
+  uint32_t* queue;
   unsigned long long* stats;  // [8]
+  // Leftover queue (two launches per frame): when a wave of the main launch first
+  // finds the unit queue dry, each of its lanes keeps the sample it is on and publishes its other
+  // unstarted samples as records of <= 2^left_sh samples (pixel, first sample, end); the leftover
+  // launch of the same kernel takes the records as its units. left_cap == 0: no records, no launch.
+  uint4* left_recs;
+  uint32_t left_cap, left_sh, left_min, sh_left;  // sh_left: guided-grab shift of the leftover launch
 };
 
 // Re-derive a wave-uniform pointer as opaque so uniform loads are re-issued (s_load) where used
@@ -268,16 +276,24 @@ using TopoGenericWide = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, true, true
 //   LREF:  1 = the reference's light sampling and RR constants (light x0/dx 32/36, z0/dz 63/36,
 //          y 81.6, area 1296 :365-367,:471; light id 6 :467; rr_depth 5 :448): literals instead
 //          of scalar loads in the loop
-template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_, int CAMAX_, int LREF_ = 0>
+//   LEAK:  1 = contract v6's leak-end rule (a leaked path ends at its first miss; the host proves
+//          it applies, leak_end_of), 0 = leaked paths go on from the miss vertex as the reference's
+//          (SPT_FLAG_REFERENCE_LEAKS, or a scene the rule does not hold for), -1 = KParams::leak_end
+template <int NEE_, int LMODE_, int BLACK_, int MAXD0_, int NOS1_, int CAMAX_, int LREF_ = 0,
+          int LEAK_ = -1>
 struct Cfg {
   static constexpr int NEE = NEE_, LMODE = LMODE_, BLACK = BLACK_, MAXD0 = MAXD0_, NOS1 = NOS1_;
-  static constexpr int CAMAX = CAMAX_, LREF = LREF_;
+  static constexpr int CAMAX = CAMAX_, LREF = LREF_, LEAK = LEAK_;
 };
 using CfgRuntime = Cfg<-1, -1, -1, -1, -1, -1>;
-using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1>;  // C3/C4: the reference's HEAD estimator
-using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1>;  // C2: cosine-weighted only
+// C3/C4: the reference's HEAD estimator; C2: cosine-weighted only (leak-end rule / reference leaks)
+using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 1>;
+using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 1>;
+using CfgHeadNeeRef = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 0>;
+using CfgHeadCosRef = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 0>;
 // Sphere scenes with the reference's NEE estimator and black light (C5): early NEE resolve
-using CfgSphNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, -1, -1, -1, 1>;
+using CfgSphNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, -1, -1, -1, 1, 1>;
+using CfgSphNeeRef = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, -1, -1, -1, 1, 0>;
 // The LREF constants (the host checks spt_params against them before it picks an LREF kernel).
 constexpr int kRefLightId = 6, kRefRrDepth = 5;
 constexpr float kRefLx0 = 32.0f, kRefLz0 = 63.0f, kRefLy = 81.6f, kRefLarea = 1296.0f;
@@ -811,6 +827,25 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// A unit index -> its (spread) local pixel, as the refill maps it (chunk-major units, pixel order
+// spread by scr_k).
+__device__ __forceinline__ uint32_t unit_pixel(const SPT_CONST KParams* Q, uint32_t u) {
+  const uint32_t r = u - div_magic(u, Q->m_npix, Q->sh_npix) * (uint32_t)Q->n_local_pix;
+  return (r & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (r >> Q->scr_k);
+}
+
+// Exclusive prefix sum over the wave (all 64 lanes active) and the wave's total.
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t& total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o);
+    x += lane >= (uint32_t)o ? y : 0u;
+  }
+  total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  return x - v;
+}
+
 
 // One lane = one pixel-sample path at a time, and every iteration traces exactly ONE ray per lane
 // with the same nearest-hit loop (intersect :323-335): either the path ray toward the next vertex
@@ -825,7 +860,9 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
 // The lane state is one VGPR word (kSt*) and the small blocks are branch-free: the loop is bound
 // by instruction issue, and LLVM's exec-mask bookkeeping for loop-carried booleans and short
 // branches was SALU work on the CU's single scalar unit.
-template <class TP, class CF>
+//   PH: 0 = the main launch (units from the queue; publishes leftover records when left_cap != 0),
+//   1 = the leftover launch (units = the records the main launch published).
+template <class TP, class CF, int PH>
 // SGPRs capped at 80: with 81-96 SGPRs a CU admits only 7 blocks of 256 threads, not the 8 that the
 // compiler's occupancy report and hipOccupancyMaxActiveBlocksPerMultiprocessor() claim (MI355X_MICROARCH
 // "256-thread blocks are admitted per CU up to min(API, 8, floor(800 / (ceil(sgpr/16)*16 + 16)))";
@@ -854,6 +891,9 @@ render_kernel(const KParams* __restrict__ Pg) {
   if (TP::SPH && threadIdx.x < kBlock / 64) s_nsph[threadIdx.x] = 0;
   // Shadow rays resolved early, per wave, in the sphere kernels (same reason: no VGPR counter)
   __shared__ uint32_t s_nearly[TP::SPH ? kBlock / 64 : 1];
+  // Main launch: the end of the range each lane parked for the leftover launch (0: none)
+  __shared__ uint32_t s_left[PH == 0 ? kBlock : 1];
+  if (PH == 0) s_left[threadIdx.x] = 0u;
   if (TP::SPH && threadIdx.x < kBlock / 64) s_nearly[threadIdx.x] = 0;
   {
     const SPT_CONST KParams* P = cptr(Pg);
@@ -906,6 +946,12 @@ render_kernel(const KParams* __restrict__ Pg) {
               C->cam_cv[1], C->cam_l[0], C->cam_l[1], C->cam_l[2], C->fix_scale};
   }
   uint32_t pool_next = 0, pool_end = 0, grab_at = 0;  // grab_at: the wave's last queue position
+  // The leftover launch's units: the records the main launch wrote (a kernel boundary lies between)
+  uint32_t n_left = 0;
+  if constexpr (PH == 1) {
+    const SPT_CONST KParams* Q = cptr(Pg);
+    n_left = (uint32_t)__builtin_amdgcn_readfirstlane((int)min(Q->queue[32], Q->left_cap));
+  }
   bool exhausted = false, capped = false;
   // Wave-uniform event counters (SGPRs), fed by ballots at convergent points of the loop: per-lane
   // counters incremented inside the divergent blocks cost ~40 VGPRs of copies.
@@ -962,42 +1008,66 @@ render_kernel(const KParams* __restrict__ Pg) {
     while (need != 0 && !exhausted) {
       SPT_REGION(2);
       const SPT_CONST KParams* Q = cptr(Pg);
+      const uint32_t n_units = PH == 1 ? n_left : Q->n_units;
       if (pool_next >= pool_end) {
         uint32_t want = kGrab;
-        if (Q->sh_guided < 32u) {
-          const uint32_t left = Q->n_units - min(grab_at, (uint32_t)Q->n_units);
-          want = min(kGrab, max(max((uint32_t)__popcll(need), kGrabMin), left >> Q->sh_guided));
+        if (PH == 1 || Q->sh_guided < 32u) {
+          const uint32_t left = n_units - min(grab_at, n_units);
+          want = min(kGrab, max(max((uint32_t)__popcll(need), kGrabMin),
+                                left >> (PH == 1 ? Q->sh_left : Q->sh_guided)));
         }
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(Q->queue, want);
+        if (lane == 0) b = atomicAdd(Q->queue + (PH == 1 ? 16 : 0), want);
         b = __builtin_amdgcn_readfirstlane(b);
         grab_at = b + want;
-        if (b >= Q->n_units) { exhausted = true; break; }
+        if (b >= n_units) {
+          exhausted = true;
+          // The main launch's leftover: the queue is dry, so each lane keeps only
+          // the sample it is on and parks the end of its range in LDS; after the loop (where few
+          // registers are live) the rest becomes records for the leftover launch, which spreads it
+          // over the whole chip -- the young waves that the SIMD's age-first issue order starves
+          // would otherwise drain it alone. Once per wave; a lane with fewer than left_min unstarted
+          // samples keeps them.
+          if (PH == 0 && Q->left_cap != 0) {
+            const bool pub = ls != kStIdle && s_end >= s + 1u + Q->left_min;
+            s_left[threadIdx.x] = pub ? s_end : 0u;
+            s_end = pub ? s + 1u : s_end;
+          }
+          break;
+        }
         pool_next = b;
-        pool_end = min(b + want, Q->n_units);
+        pool_end = min(b + want, n_units);
       }
       const uint32_t rank = lane_rank(need);
       const uint32_t avail = pool_end - pool_next;
       if (needs_unit && rank < avail) {
         const uint32_t u = pool_next + rank;
-        const uint32_t npix = (uint32_t)Q->n_local_pix, w = (uint32_t)Q->width;
-        const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major
-        lp = u - j * npix;
-        // Spread the pixel order (scr_k > 0): unit pixel lp = b * K + a -> a * (npix / K) + b, so a
-        // wave's run of consecutive units samples the whole image instead of one row segment, and
-        // per-wave work varies less (the image does not change: every pixel-sample is still done
-        // once and summed in integers)
-        lp = (lp & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (lp >> Q->scr_k);
-        s = j * (uint32_t)Q->chunk;
-        s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
-        (void)w;
-        pixel_terms(Q, lp, pk, fx, fy);
+        if constexpr (PH == 1) {  // a leftover record: pixel, first sample, end (no slot: atomics)
+          const uint4 rc = Q->left_recs[u];
+          lp = rc.x;
+          s = rc.y;
+          s_end = rc.z;
+          pixel_terms(Q, lp, pk, fx, fy);
+        } else {
+          const uint32_t npix = (uint32_t)Q->n_local_pix;
+          const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major
+          lp = u - j * npix;
+          // Spread the pixel order (scr_k > 0): unit pixel lp = b * K + a -> a * (npix / K) + b, so a
+          // wave's run of consecutive units samples the whole image instead of one row segment, and
+          // per-wave work varies less (the image does not change: every pixel-sample is still done
+          // once and summed in integers)
+          lp = (lp & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (lp >> Q->scr_k);
+          s = j * (uint32_t)Q->chunk;
+          s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
+          pixel_terms(Q, lp, pk, fx, fy);
+        }
         if constexpr (CF::CAMAX == 1) {  // the per-pixel P_x, P_y of the camera ray (jitter_f)
           fx = fmaf(ck.aux, fx, ck.lx);
           fy = fmaf(ck.avy, fy, ck.ly);
         }
 #if SPT_UNIT_SLOTS
-        lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
+        if constexpr (PH == 0)
+          lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
 #endif
         ls = kStCam;
         needs_unit = false;
@@ -1027,12 +1097,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           const uint32_t mid = dcur + (dend - dcur) / 2u;  // donor keeps [.., mid), taker [mid, dend)
           uint32_t d_lp = (uint32_t)__builtin_amdgcn_readlane((int)lp, dl);
 #if SPT_UNIT_SLOTS
-          if (d_lp >> 31) {  // an owner donor holds its unit index: the taker adds by pixel
-            const SPT_CONST KParams* Q = cptr(Pg);
-            const uint32_t du = d_lp & 0x7FFFFFFFu;
-            const uint32_t r = du - div_magic(du, Q->m_npix, Q->sh_npix) * (uint32_t)Q->n_local_pix;
-            d_lp = (r & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (r >> Q->scr_k);
-          }
+          if (d_lp >> 31)  // an owner donor holds its unit index: the taker adds by pixel
+            d_lp = unit_pixel(cptr(Pg), d_lp & 0x7FFFFFFFu);
 #endif
           const uint32_t d_qhi = (uint32_t)__builtin_amdgcn_readlane((int)pk.qhi, dl);
           const uint32_t d_qlo = (uint32_t)__builtin_amdgcn_readlane((int)pk.qlo, dl);
@@ -1198,9 +1264,9 @@ render_kernel(const KParams* __restrict__ Pg) {
           if constexpr (TP::CONSTGEO) ia = kxy ? inv.z : (kxz ? inv.y : inv.x);  // (= ia_hit)
           const float tr = hit_plane_t(n_, da, ia, plane_t(n_, ia));  // the winner's t, corrected
           x = mk(keep(o.x + d.x * tr), keep(o.y + d.y * tr), keep(o.z + d.z * tr));
-          // a miss vertex is the origin (:373-374); a leaked path ending at its miss (every LREF
-          // kernel, see below) never reads it
-          if constexpr (CF::LREF != 1) x = hit ? x : mk(0, 0, 0);
+          // a miss vertex is the origin (:373-374); a leaked path ending at its miss (the LEAK == 1
+          // kernels, see below) never reads it
+          if constexpr (CF::LEAK != 1) x = hit ? x : mk(0, 0, 0);
           if constexpr (!kEarly) l_miss += hit ? 0u : 1u;
           const float sg = da < 0.0f ? 1.0f : -1.0f;
           nl = mk(kyz ? sg : 0.0f, kxz ? sg : 0.0f, kxy ? sg : 0.0f);
@@ -1255,8 +1321,8 @@ render_kernel(const KParams* __restrict__ Pg) {
         const bool rr = (depth > rr_depth_of<CF>(P)) | (rr_t < 0);   // p == 0
         const bool alive = (int)u16i(rl.x, rl.y) < rr_t;              // (p > 0) & (p >= 1 | u16 < p)
         // contract v6: a leaked path ends at its first miss (host leak_end_of, oracle
-        // c_find_leak_end); the host launches the LREF kernels only where that rule holds
-        const bool leak = CF::LREF == 1 || P->leak_end != 0;
+        // c_find_leak_end); the host launches the LEAK == 1 kernels only where that rule holds
+        const bool leak = CF::LEAK == 1 || (CF::LEAK < 0 && P->leak_end != 0);
         const bool term = capd | (rr & !alive) | (!hit & leak);
         const float ip = keep(H.ip);  // == 1.0f / p, read unconditionally (no branch)
         const float fsc = rr ? ip : 1.0f;
@@ -1492,6 +1558,27 @@ render_kernel(const KParams* __restrict__ Pg) {
     reg_flags = 0;
 #endif
   }
+  if constexpr (PH == 0) {  // publish the parked ranges: every lane is idle, at s = its kept end
+    const SPT_CONST KParams* Q = cptr(Pg);
+    const uint32_t end = s_left[threadIdx.x];
+    bool lost = false;
+    if (Q->left_cap != 0 && end > s) {
+      const uint32_t piece = 1u << Q->left_sh;
+      const uint32_t nrec = (end - s + piece - 1u) >> Q->left_sh;
+      // one atomic per lane (the atomic optimizer scans them into one per wave)
+      const uint32_t base = atomicAdd(Q->queue + 32, nrec);
+      // (the host sizes left_recs for every lane's whole unit: the check never fails)
+      if (base + nrec <= Q->left_cap) {
+        const uint32_t px = (lp >> 31) ? unit_pixel(Q, lp & 0x7FFFFFFFu) : lp;
+        uint4* out = Q->left_recs + base;
+        for (uint32_t a = s, i = 0; i < nrec; ++i, a += piece)
+          out[i] = uint4{px, a, min(a + piece, end), 0u};
+      } else {
+        lost = true;  // cannot happen; if it did, report an incomplete image, never a wrong one
+      }
+    }
+    if (__ballot(lost) != 0) capped = true;
+  }
   {
     unsigned long long* st = cptr(Pg)->stats;  // wave-reduced by the atomic optimizer
 #ifdef SPT_WAVE_TIMES
@@ -1507,8 +1594,9 @@ render_kernel(const KParams* __restrict__ Pg) {
       atomicAdd(st + 18, wave_t0 >> 4);  // sums of start / end times (/16: no overflow)
       atomicAdd(st + 19, t1 >> 4);
       atomicAdd(st + 20, (unsigned long long)__smid());
-      const uint32_t wid = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-      if (wid < 32768) {
+      // the leftover launch's waves from entry 16384 on (tools/wave_tail.py splits there)
+      const uint32_t wid = blockIdx.x * (kBlock / 64) + threadIdx.x / 64 + (PH == 1 ? 16384u : 0u);
+      if (wid < (PH == 1 ? 32768u : 16384u)) {
         st[32 + 3 * wid] = wave_t0;
         st[33 + 3 * wid] = t1;
         st[34 + 3 * wid] = ((unsigned long long)__smid() << 32) | wave_iters;
@@ -1530,7 +1618,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       atomicAdd(st + 3, np);  // + the light hits, added per lane below
       atomicAdd(st + 6, (unsigned long long)n_cos);
     }
-    if (!TP::MAT && blockIdx.x == 0 && threadIdx.x == 0) {  // one camera ray per sample
+    if (!TP::MAT && PH == 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // one camera ray per sample
       const SPT_CONST KParams* C = cptr(Pg);
       const unsigned long long samples = (unsigned long long)C->n_local_pix * (unsigned long long)C->spp;
       atomicAdd(st + 1, samples);
@@ -1627,18 +1715,41 @@ static spt_status fail(spt_status s, const std::string& msg) {
 // level).
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
-       KV_SPHDIFF_NEE, KV_RECTDIFF, KV_COUNT };
-static const RenderFn kRenderKernels[KV_COUNT] = {
-    render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
-    render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
-    render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>,
-    render_kernel<TopoGenericWide, CfgRuntime>, render_kernel<TopoSphDiff, CfgSphNee>,
-    render_kernel<TopoRectDiff, CfgRuntime>};
+       KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF, KV_COUNT };
+template <int PH>
+static constexpr RenderFn kRenderKernelsOf[KV_COUNT] = {
+    render_kernel<TopoGeneric, CfgRuntime, PH>, render_kernel<TopoCornell, CfgRuntime, PH>,
+    render_kernel<TopoCornellConst, CfgRuntime, PH>, render_kernel<TopoCornellConst, CfgHeadNee, PH>,
+    render_kernel<TopoCornellConst, CfgHeadCos, PH>, render_kernel<TopoSphDiff, CfgRuntime, PH>,
+    render_kernel<TopoGenericWide, CfgRuntime, PH>, render_kernel<TopoSphDiff, CfgSphNee, PH>,
+    render_kernel<TopoRectDiff, CfgRuntime, PH>, render_kernel<TopoCornellConst, CfgHeadNeeRef, PH>,
+    render_kernel<TopoCornellConst, CfgHeadCosRef, PH>, render_kernel<TopoSphDiff, CfgSphNeeRef, PH>};
+static const RenderFn* const kRenderKernels = kRenderKernelsOf<0>;     // the main launch
+static const RenderFn* const kLeftoverKernels = kRenderKernelsOf<1>;   // the leftover launch
+
+// Leftover queue settings, read once per context from the environment for A/B runs:
+// SPT_LEFTOVER=1 turns it on (A/B: it lost on C2 and C3); SPT_LEFT_PIECE = samples per
+// record (a power of two); SPT_LEFT_MIN = fewest unstarted samples a lane publishes.
+#ifndef SPT_LEFT_PIECE
+#define SPT_LEFT_PIECE 16
+#endif
+#ifndef SPT_LEFT_MIN
+#define SPT_LEFT_MIN 4
+#endif
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
 
 struct spt_context {
   int device = 0;
   int n_cu = 0, blocks_per_cu = 0;      // generic kernel
   int bpc[KV_COUNT] = {};               // resident blocks per CU of each variant
+  int bpc_left[KV_COUNT] = {};          // ... and of its leftover-launch form
+  bool leftover = false;                // SPT_LEFTOVER (default off)
+  uint32_t left_sh = 4, left_min = 4;   // log2 samples per record; fewest samples published
+  uint4* left_recs = nullptr;           // leftover records, grown on demand
+  size_t left_recs_cap = 0;             // records
   DevPrim* prims = nullptr;
   SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
@@ -1681,7 +1792,7 @@ static spt_status validate(const spt_prim* prims, int32_t n, const spt_camera* c
   if (p->shard_count < 1 || p->shard_index < 0 || p->shard_index >= p->shard_count)
     return fail(SPT_ERR_INVALID_ARG, "bad shard_index/shard_count");
   if (p->tile_rows < 0 || p->chunk < 0) return fail(SPT_ERR_INVALID_ARG, "negative tile/chunk");
-  if (p->flags & ~(SPT_FLAG_UNIFORM_SCATTER | SPT_FLAG_KERNEL_LEVEL_MASK))
+  if (p->flags & ~(SPT_FLAG_UNIFORM_SCATTER | SPT_FLAG_REFERENCE_LEAKS | SPT_FLAG_KERNEL_LEVEL_MASK))
     return fail(SPT_ERR_INVALID_ARG, "unknown flags");
   if (((p->flags & SPT_FLAG_KERNEL_LEVEL_MASK) >> 8) > SPT_KERNEL_LEVEL_CONST)
     return fail(SPT_ERR_INVALID_ARG, "bad kernel level");
@@ -2009,8 +2120,20 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
             hipSuccess || bpc <= 0)
       bpc = 4;
     c->bpc[v] = bpc;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kLeftoverKernels[v], kBlock, 0) !=
+            hipSuccess || bpc <= 0)
+      bpc = 4;
+    c->bpc_left[v] = bpc;
   }
   c->blocks_per_cu = c->bpc[KV_GENERIC];
+  c->leftover = env_int("SPT_LEFTOVER", 0) != 0;
+  {
+    const int piece = std::max(1, std::min(1 << 20, env_int("SPT_LEFT_PIECE", SPT_LEFT_PIECE)));
+    uint32_t sh = 0;
+    while ((1 << (sh + 1)) <= piece) ++sh;
+    c->left_sh = sh;
+    c->left_min = (uint32_t)std::max(1, env_int("SPT_LEFT_MIN", SPT_LEFT_MIN));
+  }
   hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
   if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
@@ -2043,6 +2166,7 @@ extern "C" spt_status spt_context_destroy(spt_context* c) {
   if (c->h_kp) (void)hipHostFree(c->h_kp);
   if (c->accum) (void)hipFree(c->accum);
   if (c->slots) (void)hipFree(c->slots);
+  if (c->left_recs) (void)hipFree(c->left_recs);
   if (c->queue) (void)hipFree(c->queue);
   if (c->stats) (void)hipFree(c->stats);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -2152,26 +2276,28 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const bool lref = p->rr_depth == kRefRrDepth && p->light_id == kRefLightId &&
                     p->light_x0 == kRefLx0 && p->light_dx == 36.0f && p->light_z0 == kRefLz0 &&
                     p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
-  K.leak_end = leak_end_of(prims, n_prims, g);
+  K.leak_end = (p->flags & SPT_FLAG_REFERENCE_LEAKS) ? 0 : leak_end_of(prims, n_prims, g);
+  // (each estimator kernel in two forms: the leak-end rule, or leaked paths as the reference's)
   const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
-                        p->rr_depth >= 1 && cam_axis && lref && K.leak_end;
+                        p->rr_depth >= 1 && cam_axis && lref;
   int kv = g.n_sph_wide > 0 ? KV_WIDE : KV_GENERIC;  // (only the wide kernel has the fp64 loop)
-  if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CONST_NEE;
-  else if (head_est && p->nee_prob <= 0.0f) kv = KV_CONST_COS;
+  if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP)
+    kv = K.leak_end ? KV_CONST_NEE : KV_CONST_NEE_REF;
+  else if (head_est && p->nee_prob <= 0.0f) kv = K.leak_end ? KV_CONST_COS : KV_CONST_COS_REF;
   else if (cconst) kv = KV_CONST;
   else if (cornell) kv = KV_CORNELL;
   else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
     kv = g.n_sph == 0 ? KV_RECTDIFF
-         : kcap >= 3 && K.light_black && lref && K.leak_end && p->nee_prob >= 1.0f &&
+         : kcap >= 3 && K.light_black && lref && p->nee_prob >= 1.0f &&
                  p->light_mode == SPT_LIGHT_GLIBC_WRAP && light_pos >= 0 &&
                  prims[p->light_id].kind == SPT_RECT_XZ
-             ? KV_SPHDIFF_NEE
+             ? (K.leak_end ? KV_SPHDIFF_NEE : KV_SPHDIFF_NEE_REF)
              : KV_SPHDIFF;
   // The sphere NEE kernel's early resolve needs the HEAD room (rect[] :287-294, light at index 6)
   // as prims 0..6, nothing else but narrow spheres, and a threshold above every sphere's top
   // (early_room_proven); otherwise it stays off (+inf) and every shadow ray is traced.
   K.early_y0 = INFINITY;
-  if (kv == KV_SPHDIFF_NEE && n_prims > 7 && g.n_sph_wide == 0) {
+  if ((kv == KV_SPHDIFF_NEE || kv == KV_SPHDIFF_NEE_REF) && n_prims > 7 && g.n_sph_wide == 0) {
     spt_prim head[17];
     int32_t nh = 0;
     bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
@@ -2233,6 +2359,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 #define SPT_GUIDED_ALL 0  // A/B: guided grabs for long launches too
 #endif
     K.sh_guided = (small_launch || SPT_GUIDED_ALL) ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
+    // the leftover launch always grabs guided (its records are few and short)
+    const uint32_t waves_l = (uint32_t)(c->n_cu * c->bpc_left[kv] * (kBlock / 64));
+    uint32_t shl = 1;
+    while ((1u << shl) < 2u * waves_l && shl < 31) ++shl;
+    K.sh_left = std::min(31u, shl + (uint32_t)SPT_GUIDED_EXTRA);
   }
   K.chunk = chunk;
   K.steal_min = small_launch ? SPT_STEAL_MIN_SMALL : SPT_STEAL_MIN;
@@ -2283,6 +2414,27 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   K.slots = c->slots;
   K.queue = c->queue;
   K.stats = c->stats;
+  // Leftover records: at most one lane's unit less its current sample per resident lane of the
+  // main launch, in records of 2^left_sh samples (C3: 524 288 lanes x 6 records x 16 B = 50 MB).
+  const int grid = c->n_cu * c->bpc[kv];
+  K.left_cap = 0;
+  K.left_sh = c->left_sh;
+  K.left_min = c->left_min;
+  if (c->leftover && (uint32_t)chunk > c->left_min) {
+    const uint64_t per_lane = ((uint64_t)chunk - 1 + (1u << c->left_sh) - 1) >> c->left_sh;
+    const uint64_t cap = (uint64_t)grid * kBlock * per_lane;
+    if (cap < 0x80000000ull) {
+      if (cap > c->left_recs_cap) {
+        if (c->left_recs) SPT_HIP(hipFree(c->left_recs));
+        c->left_recs = nullptr;
+        c->left_recs_cap = 0;
+        SPT_HIP(hipMalloc(&c->left_recs, cap * sizeof(uint4)));
+        c->left_recs_cap = cap;
+      }
+      K.left_cap = (uint32_t)cap;
+    }
+  }
+  K.left_recs = c->left_recs;
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
   K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
@@ -2300,19 +2452,24 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 
   SPT_HIP(hipMemsetAsync(c->accum, 0, sizeof(unsigned long long) * 3 * (size_t)K.n_local_pix,
                          stream));
-  SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream));
+  SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t) * 64, stream));  // unit + leftover queues
   SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
 #ifdef SPT_WAVE_TIMES
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
-  c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE;
-  const int grid = c->n_cu * c->bpc[kv];
+  c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
+                       kv == KV_SPHDIFF_NEE_REF;
   *c->h_kp = K;
   SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   SPT_HIP(hipEventRecord(c->ev0, stream));
   hipLaunchKernelGGL(kRenderKernels[kv], dim3(grid), dim3(kBlock), 0, stream,
                      (const KParams*)c->d_kp);
   SPT_HIP(hipGetLastError());
+  if (K.left_cap != 0) {  // the leftover launch: the same kernel over the published records
+    hipLaunchKernelGGL(kLeftoverKernels[kv], dim3(c->n_cu * c->bpc_left[kv]), dim3(kBlock), 0,
+                       stream, (const KParams*)c->d_kp);
+    SPT_HIP(hipGetLastError());
+  }
   SPT_HIP(hipEventRecord(c->ev1, stream));
 #if SPT_UNIT_SLOTS
   const uint32_t np = (uint32_t)K.n_local_pix;

@@ -231,12 +231,15 @@ def test_full_size_configs_rows_bit_exact(spt, oracle, cfg):
     _assert_exact(gpu[rows], cpu)
 
 
-@pytest.mark.parametrize("seed", [1, 5])
-def test_early_nee_resolve_matches_oracle_proof(spt, oracle, seed):
+@pytest.mark.parametrize("seed,ref_leaks", [(1, False), (5, False), (2, True)])
+def test_early_nee_resolve_matches_oracle_proof(spt, oracle, seed, ref_leaks):
     """The HEAD NEE kernel resolves the shadow rays early_nee_proven() covers without tracing them.
     The image and path statistics stay bit-exact, and the number of rays it resolved that way
-    equals the oracle's count of the same claims, none of which its own intersect contradicts."""
-    p = spt.default_params(width=256, height=192, spp=32, seed=seed)
+    equals the oracle's count of the same claims, none of which its own intersect contradicts.
+    ref_leaks: leaked paths go on as the reference's (SPT_FLAG_REFERENCE_LEAKS), so vertices on the
+    walls' outer faces and at the miss vertex take NEE samples too."""
+    p = spt.default_params(width=256, height=192, spp=32, seed=seed,
+                           flags=spt.FLAG_REFERENCE_LEAKS if ref_leaks else 0)
     oracle.proof_check(True)
     try:
         gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
@@ -250,11 +253,13 @@ def test_early_nee_resolve_matches_oracle_proof(spt, oracle, seed):
     assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
 
 
-def test_early_nee_resolve_spheres_matches_oracle_proof(spt, oracle):
+@pytest.mark.parametrize("ref_leaks", [False, True])
+def test_early_nee_resolve_spheres_matches_oracle_proof(spt, oracle, ref_leaks):
     """The sphere NEE kernel (C5's scene and estimator, depth cap 16) resolves the shadow rays of
     vertices above every sphere's top + 1 (y0 = 13) early: bit-exact image and statistics, and the
-    same count as the oracle's claims, none contradicted."""
-    p = spt.default_params(width=128, height=96, spp=16, seed=9, max_depth=16)
+    same count as the oracle's claims, none contradicted (also with the reference's leaked paths)."""
+    p = spt.default_params(width=128, height=96, spp=16, seed=9, max_depth=16,
+                           flags=spt.FLAG_REFERENCE_LEAKS if ref_leaks else 0)
     oracle.proof_check(True, sphere_y0=13.0)
     try:
         gpu, gst, cpu, cst = _render_both(spt, oracle, spt.spheres32_scene(), p)
@@ -507,3 +512,43 @@ def test_leak_end_off_when_the_miss_vertex_emits(spt, oracle, nee):
     _assert_exact(gpu, cpu)
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
     assert gst["misses"] / gst["samples"] > 0.1  # the reference's repeated misses, not first ones
+
+
+@pytest.mark.parametrize("kernel", ["head", "const", "generic"])
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_reference_leaks_flag_bit_exact(spt, oracle, kernel, nee):
+    """SPT_FLAG_REFERENCE_LEAKS: the HEAD scene with leaked paths going on from the miss
+    vertex as the reference's (:371-377) instead of ending at their first miss (contract v6) -- on the
+    estimator kernels' reference-leak forms, the run-time kernel and the generic one. Image and
+    statistics equal the oracle's with the same flag, and the oracle's with its leak-end rule switched
+    off by the test hook (set_leak_end(False)) without it."""
+    fl = spt.FLAG_REFERENCE_LEAKS | spt.kernel_flag(kernel)
+    p = spt.default_params(width=64, height=48, spp=16, seed=1, nee_prob=nee, flags=fl)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, spt.cornell_scene(), p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    p0 = spt.default_params(width=64, height=48, spp=16, seed=1, nee_prob=nee,
+                            flags=spt.kernel_flag(kernel))
+    cam = spt.Camera(aspect=64 / 48)
+    oracle.set_leak_end(False)
+    try:
+        cpu0, cst0 = oracle.counter_render(spt.cornell_scene(), cam._c, p0)
+    finally:
+        oracle.set_leak_end(True)
+    _assert_exact(gpu, cpu0)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst0
+    # the reference's repeated misses (a leaked path re-misses from the origin), not first ones
+    _, first = spt.render(spt.cornell_scene(), cam, p0, return_stats=True)
+    assert gst["misses"] > 2 * first["misses"]
+    assert gst["vertices"] > first["vertices"]
+
+
+def test_reference_leaks_c3_rows_bit_exact(spt, oracle):
+    """C3's size and spp with SPT_FLAG_REFERENCE_LEAKS, on a spread subset of its rows (the leftover
+    launch and the reference-leak HEAD NEE kernel at full size)."""
+    p = spt.default_params(width=1024, height=768, spp=512, seed=1, flags=spt.FLAG_REFERENCE_LEAKS)
+    cam = spt.Camera(aspect=float(np.float32(1024) / np.float32(768)))
+    gpu = spt.render(spt.cornell_scene(), cam, p)
+    rows = np.array([0, 191, 383, 384, 600, 767])
+    cpu, _ = oracle.counter_render(spt.cornell_scene(), cam._c, p, rows=rows)
+    _assert_exact(gpu[rows], cpu)

@@ -271,6 +271,33 @@ def test_early_nee_resolve_proof_holds(oracle, pairs):
     assert claims > 0.55 * st["nee_light_hits"], (claims, st["nee_light_hits"])
 
 
+def test_early_nee_resolve_proof_holds_with_reference_leaks(oracle, spt):
+    """SPT_FLAG_REFERENCE_LEAKS: leaked paths wander on from the miss vertex (the origin) and across
+    the walls' outer faces as the reference's (:371-377), and those vertices take NEE samples too.
+    The HEAD NEE kernel's early resolve must still never claim a shadow ray its intersect would not
+    give the light; and the flag is the test hook's set_leak_end(False), bit for bit."""
+    prims = oracle.scene_cornell()
+    w, h, spp = 192, 144, 32
+    p = oracle.default_params(width=w, height=h, spp=spp, seed=13, flags=spt.FLAG_REFERENCE_LEAKS)
+    oracle.proof_check(True)
+    try:
+        img, st = oracle.counter_render(prims, oracle.camera(w / h), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    assert bad == 0, (claims, bad)
+    assert claims > 0.55 * st["nee_light_hits"], (claims, st["nee_light_hits"])
+    p0 = oracle.default_params(width=w, height=h, spp=spp, seed=13)
+    oracle.set_leak_end(False)
+    try:
+        img0, st0 = oracle.counter_render(prims, oracle.camera(w / h), p0)
+    finally:
+        oracle.set_leak_end(True)
+    assert np.array_equal(img, img0) and st == st0
+    img1, st1 = oracle.counter_render(prims, oracle.camera(w / h), p0)
+    assert st["misses"] > 2 * st1["misses"] and not np.array_equal(img, img1)
+
+
 def test_early_nee_resolve_proof_holds_spheres(oracle, spt):
     """The sphere NEE kernel's early resolve (early_room_proven: the HEAD room, vertices above
     every sphere's top + 1 = 13 in the C5 scene) against the contract's intersect, depth cap 16."""
