@@ -61,9 +61,13 @@ def host_threads() -> int:
 
 
 QUALITY_FIXTURE = os.path.join(ROOT, "tests", "golden", "ref_c3_blocks_k32.npz")
+# per config: the fixture and the reference binary its runs came from (tests/golden/make_golden.py
+# --quality-c3 / --quality-c2)
+QUALITY_FIXTURES = {"c3": (QUALITY_FIXTURE, "smallpt_nee_xs"),
+                    "c2": (os.path.join(ROOT, "tests", "golden", "ref_c2_blocks_k32.npz"), "smallpt_cos_xs")}
 
 
-def quality(img: np.ndarray, spp: int, extra_images=()):
+def quality(img: np.ndarray, spp: int, extra_images=(), config: str = "c3"):
     """The metric's quality half (BASELINE.json: per-channel RMSE vs the reference PPM) at C3:
     the GPU image, quantised and linearised as the reference's P3 (toInt :319-321, (v/255)^2.2),
     as 32x32-block means against the pooled block means of 16 independent runs of the reference
@@ -76,10 +80,13 @@ def quality(img: np.ndarray, spp: int, extra_images=()):
     seed 1). Pooled with it, they give the comparison at a matched budget -- as many 512-spp runs
     on each side -- whose noise floor is below the north star's 1e-3 tolerance. (Runs are pooled
     rather than rendered at 16x the spp: the per-pixel clamp of :538 makes an image depend on its
-    own spp.)"""
-    if not os.path.exists(QUALITY_FIXTURE):
+    own spp.)
+    config "c2": the same against 16 runs of oracle/_ref/smallpt_cos_xs at C2's 1024x768 @ 64 spp
+    (tests/golden/ref_c2_blocks_k32.npz)."""
+    fixture, ref_bin = QUALITY_FIXTURES[config]
+    if not os.path.exists(fixture):
         return None
-    f = np.load(QUALITY_FIXTURE)  # plain arrays (allow_pickle=False)
+    f = np.load(fixture)  # plain arrays (allow_pickle=False)
     blocks, (w, h, spp_ref, k) = f["blocks"], [int(v) for v in f["shape"]]
     if img.shape != (h, w, 3):
         return None
@@ -118,8 +125,8 @@ def quality(img: np.ndarray, spp: int, extra_images=()):
             "rmse_vs_contract": None,
             "matched_budget": matched,
             "space": f"linear, quantised as the reference's P3, {k}x{k}-block means, per channel (R,G,B)",
-            "reference": f"{n} runs of oracle/_ref/smallpt_nee_xs at {w}x{h} @ {spp_ref} spp "
-                         f"({n * spp_ref} spp pooled), tests/golden/{os.path.basename(QUALITY_FIXTURE)}"}
+            "reference": f"{n} runs of oracle/_ref/{ref_bin} at {w}x{h} @ {spp_ref} spp "
+                         f"({n * spp_ref} spp pooled), tests/golden/{os.path.basename(fixture)}"}
 
 
 def cpu_baseline(spt, prims, cam, params, gpu_img, budget_s: float):
@@ -269,22 +276,37 @@ def launch_ranks(n: int, argv, timeout_s: float, env=None) -> int:
     one rank per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR = 127.0.0.1, a free
     MASTER_PORT), and wait for them. The parent never touches the GPU (no torch import, no HIP
     call): it only starts processes, so nothing is exec'd from a process that initialised the GPU.
-    The children inherit stdout, so rank 0's JSON line is the parent's output (the other ranks print
-    none). Returns 0 when every rank exits 0. Otherwise it returns the first failing rank's status
+    The parent reads every child's stdout: rank 0's JSON lines are its own stdout, everything else
+    (gloo's connection messages, which it prints on stdout) goes to stderr, so the parent's stdout
+    holds exactly the one JSON line. Returns 0 when every rank exits 0. Otherwise it returns the first failing rank's status
     (124 when the ranks outlive `timeout_s`), after ending the remaining children: each runs in its
     own process group, and the parent kills exactly those groups. No retry.
     The reference's own parallel construct is an OpenMP pragma over rows (smallpt.cpp:526-528)."""
     import signal
     import subprocess
+    import threading
 
     base = dict(os.environ if env is None else env)
     base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
                 MASTER_PORT=str(free_port()), SPT_BENCH_SPAWNED="1")
-    procs = []
+    procs, readers = [], []
+
+    def forward(rank, pipe):
+        for line in iter(pipe.readline, b""):
+            if rank == 0 and line.lstrip().startswith(b"{"):
+                sys.stdout.buffer.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.buffer.write(line)
+                sys.stderr.flush()
+        pipe.close()
+
     for i in range(n):
         e = dict(base, RANK=str(i), LOCAL_RANK=str(i))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
-                                      env=e, start_new_session=True))
+                                      env=e, start_new_session=True, stdout=subprocess.PIPE))
+        readers.append(threading.Thread(target=forward, args=(i, procs[-1].stdout), daemon=True))
+        readers[-1].start()
     deadline = time.monotonic() + timeout_s
     status = 0
     live = list(procs)
@@ -317,6 +339,8 @@ def launch_ranks(n: int, argv, timeout_s: float, env=None) -> int:
                     p.wait()
             break
         time.sleep(0.05)
+    for t in readers:
+        t.join(timeout=10)
     return status
 
 
@@ -337,6 +361,9 @@ def main() -> None:
     ap.add_argument("--save-ppm", default="")
     ap.add_argument("--kernel-level", default="auto", help="A/B only: cap the kernel specialisation "
                     "(auto | generic | cornell | const; spt_params.flags, never changes results)")
+    ap.add_argument("--move-box", type=float, default=0.0,
+                    help="edit rect[] (:287-311): move the short box by this many units in x (the "
+                         "HEAD topology with uploaded geometry; 0 = the reference's table)")
     ap.add_argument("--reference-leaks", action="store_true",
                     help="leaked paths go on from the miss vertex as the reference's (:371-377; "
                          "SPT_FLAG_REFERENCE_LEAKS) instead of ending at their first miss (contract v6)")
@@ -418,6 +445,9 @@ def main() -> None:
     if scaling == "weak":
         spp *= world
     prims = spt.cornell_scene() if cfg["scene"] == "cornell" else spt.spheres32_scene()
+    if args.move_box:
+        assert cfg["scene"] == "cornell", "--move-box edits the Cornell scene"
+        prims = spt.move_short_box(prims, args.move_box)
     w, h = cfg["width"], cfg["height"]
     cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
     leak_flag = spt.FLAG_REFERENCE_LEAKS if args.reference_leaks else 0
@@ -623,22 +653,41 @@ def main() -> None:
     my_samples = len(my_rows) * w * spp
     assert s0["samples"] == my_samples, (s0["samples"], my_samples)
 
-    traffic = None
+    traffic, traffic_file = None, None
     if os.path.exists(args.traffic) and args.config == "c3" and world == 1:
         try:
-            traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+            traffic_file = json.load(open(args.traffic))
+            traffic = traffic_file.get("hbm_bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
+    # Hardware-counter figures come from a committed rocprofv3 session (scripts/session.sh, copied
+    # into profiles/ by scripts/update_profiles.py), not from this run: each file records the hash
+    # of the kernel sources it profiled, and a file taken on other sources is not used.
+    this_sha = spt.kernel_sources_sha16()
+    hw_notes = []
+
+    def current_profile(pattern):
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+        if not files:
+            return None, None
+        d_ = json.load(open(files[-1]))
+        name = f"profiles/{os.path.basename(files[-1])}"
+        if d_.get("kernel_sources_sha16") != this_sha:
+            hw_notes.append(f"{name} profiled kernel sources {d_.get('kernel_sources_sha16')}, this "
+                            f"build is {this_sha}: not used")
+            return None, name
+        return d_, name
+
     pmc = {}
-    # the newest round's PMC summary (scripts/update_profiles.py)
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_summary.json")))
-    pmc_path = pmcs[-1] if pmcs else ""
-    if pmc_path and args.config == "c3" and world == 1:
+    if args.config == "c3" and world == 1:
         try:
-            der = json.load(open(pmc_path))["derived"]
-            pmc = {"valu_issue_frac": round(der["valu_issue_frac_of_peak"], 3),
-                   "valu_lane_utilization": round(der["valu_lane_utilization"], 3),
-                   "source": f"profiles/{os.path.basename(pmc_path)} (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU)"}
+            d_, name = current_profile("r[0-9][0-9]_pmc_summary.json")
+            if d_ is not None:
+                der = d_["derived"]
+                pmc = {"valu_issue_frac": round(der["valu_issue_frac_of_peak"], 3),
+                       "valu_lane_utilization": round(der["valu_lane_utilization"], 3),
+                       "source": f"{name} (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU; a committed profile "
+                                 f"session of this kernel build, not this run)"}
         except Exception:  # noqa: BLE001
             pmc = {}
 
@@ -646,18 +695,27 @@ def main() -> None:
     # C3 instruction-class passes (scripts/session.sh classes) counts FP32 operations per
     # wave-instruction; x 64 lanes x the measured lane utilisation = FLOP executed per launch
     hw = {}
-    cls = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_c3_classes.json")))
-    if cls and args.config == "c3" and world == 1:
+    if args.config == "c3" and world == 1:
         try:
-            c_ = json.load(open(cls[-1]))["counters"]
-            lu = c_["SQ_THREAD_CYCLES_VALU"] / (64.0 * c_["SQ_ACTIVE_INST_VALU"])
-            hw_flop = c_["SQ_INSTS_VALU_FLOPS_FP32"] * 64.0 * lu
-            hw = {"frac_hw": round(hw_flop / (float(kms.mean()) * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
-                  "hw_flop_per_launch": round(hw_flop, -6),
-                  "hw_source": f"profiles/{os.path.basename(cls[-1])}: SQ_INSTS_VALU_FLOPS_FP32 x 64 "
-                               f"x lane utilisation {lu:.3f} over this run's kernel time"}
+            d_, name = current_profile("r[0-9][0-9]_pmc_c3_classes.json")
+            if d_ is not None:
+                c_ = d_["counters"]
+                lu = c_["SQ_THREAD_CYCLES_VALU"] / (64.0 * c_["SQ_ACTIVE_INST_VALU"])
+                hw_flop = c_["SQ_INSTS_VALU_FLOPS_FP32"] * 64.0 * lu
+                hw = {"frac_hw": round(hw_flop / (float(kms.mean()) * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                      "hw_flop_per_launch": round(hw_flop, -6),
+                      "hw_source": f"{name}: SQ_INSTS_VALU_FLOPS_FP32 x 64 x lane utilisation {lu:.3f} "
+                                   f"over this run's kernel time",
+                      "hw_counters_from": "a committed profile session of this kernel build "
+                                          f"(kernel sources {this_sha}), not this run"}
         except Exception:  # noqa: BLE001
             hw = {}
+    if traffic_file is not None and traffic_file.get("kernel_sources_sha16") != this_sha:
+        hw_notes.append(f"{os.path.relpath(args.traffic, ROOT)} profiled kernel sources "
+                        f"{traffic_file.get('kernel_sources_sha16')}, this build is {this_sha}: not used")
+        traffic = None
+    if hw_notes:
+        hw["hw_stale"] = "; ".join(hw_notes)
 
     gather_exact = None
     if rank == 0:
@@ -669,11 +727,33 @@ def main() -> None:
             one = spt.render(prims, cam, p1)
             gather_exact = bool(np.array_equal(one, img))
             assert gather_exact, "gathered image differs from the 1-GPU render"
+        # Contract v6's leak-end rule, quantified on this workload: the same render
+        # with leaked paths going on as the reference's (SPT_FLAG_REFERENCE_LEAKS; the same Philox
+        # streams, so only the leaked paths differ), after the timed region
+        leak = None
+        if world == 1 and cfg["scene"] == "cornell":
+            if args.reference_leaks:
+                leak = {"rule": "off: leaked paths go on from the miss vertex as the reference's "
+                                "(:371-377, SPT_FLAG_REFERENCE_LEAKS)"}
+            else:
+                pr = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
+                                        max_depth=cfg["max_depth"], tile_rows=8, device=local,
+                                        flags=spt.FLAG_REFERENCE_LEAKS)
+                img_r, st_r = spt.render(prims, cam, pr, return_stats=True)
+                leak = {"rule": "contract v6: a leaked path ends at its first miss (DESIGN.md §3); "
+                                "the reference wanders on from the miss vertex (:371-377)",
+                        "reference_vertices_per_sample": round(st_r["vertices"] / my_samples, 4),
+                        "reference_vertices_skipped_frac": round(1 - s0["vertices"] / st_r["vertices"], 4),
+                        "reference_path_rays_skipped_frac": round(1 - s0["path_rays"] / st_r["path_rays"], 4),
+                        "image_mean_rel_diff": float(f"{(img.mean() - img_r.mean()) / img_r.mean():.3g}"),
+                        "how": "one render of this workload with SPT_FLAG_REFERENCE_LEAKS (same seed, "
+                               "same random streams) after the timed region"}
         cpu = None
         port = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = reference_baseline(cfg, args.cpu_budget)
-            omp = reference_baseline(cfg, args.cpu_budget, threads=host_threads())
+            # (the reference binaries hold the unedited table: no reference leg for an edited scene)
+            cpu = None if args.move_box else reference_baseline(cfg, args.cpu_budget)
+            omp = None if args.move_box else reference_baseline(cfg, args.cpu_budget, threads=host_threads())
             port = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
             if cpu is not None and omp is not None:
                 cpu["openmp"] = omp
@@ -685,12 +765,13 @@ def main() -> None:
             spt.write_ppm(args.save_ppm, img)
         writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)
         qual = None
-        if args.config == "c3" and world == 1 and os.path.exists(QUALITY_FIXTURE):
+        if (args.config in QUALITY_FIXTURES and world == 1 and not args.move_box
+                and os.path.exists(QUALITY_FIXTURES[args.config][0])):
             # 15 more seeds of the same render (after the timed region): the matched-budget RMSE
             extra = [spt.render(prims, cam, spt.default_params(
                 width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"], max_depth=cfg["max_depth"],
                 tile_rows=8, device=local, seed=sd_, flags=leak_flag)) for sd_ in range(2, 17)]
-            qual = quality(img, spp, extra)
+            qual = quality(img, spp, extra, config=args.config)
         if qual is not None and port is not None:
             # the bench's own rows re-rendered by the CPU contract (cpu_baseline.port): exact
             qual["rmse_vs_contract"] = 0.0 if port.get("gpu_pixels_bit_exact") else None
@@ -705,7 +786,9 @@ def main() -> None:
                      "32 DIFF spheres of the reference's Sphere class :223-254)")
                     + " and camera (:521), Philox4x32-7 stream seed 1",
             "config": {"workload": cfg["desc"] + (f", weak-scaled to {spp} spp over {world} GPUs"
-                                                   if scaling == "weak" and world > 1 else ""),
+                                                   if scaling == "weak" and world > 1 else "")
+                       + (f", short box moved {args.move_box:g} in x (edited rect[])" if args.move_box else "")
+                       + (", leaked paths as the reference's" if args.reference_leaks else ""),
                        "width": w, "height": h, "spp": spp,
                        "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",
                        "frames_in_flight": nfly,
@@ -749,7 +832,9 @@ def main() -> None:
                       # path leaving the room (the reference re-misses from its miss vertex,
                       # :373-374: 0.22 misses but ~0.047 leaked paths per sample at C3)
                       "misses_per_sample": round(s0["misses"] / my_samples, 4),
-                      "misses": "first misses: leaked paths end there (contract v6, DESIGN.md §3)"},
+                      "misses": ("every miss (leaked paths go on as the reference's)" if args.reference_leaks
+                                 else "first misses: leaked paths end there (contract v6, DESIGN.md §3)"),
+                      "leak_end": leak},
             "quality": qual,
             "gather_equals_1gpu_render": gather_exact,
             "gather": gather_mode,

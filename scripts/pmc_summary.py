@@ -2,10 +2,13 @@
 usage: python scripts/pmc_summary.py gpurun_out/prof_TAG [kernel-substring]"""
 import csv
 import glob
+import importlib
 import json
 import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 root = sys.argv[1]
 kname = sys.argv[2] if len(sys.argv) > 2 else "render_kernel"
@@ -20,7 +23,9 @@ for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True
         if kname in r["Kernel_Name"]:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
 avg = {k: sum(v) / len(v) for k, v in vals.items()}
-out = {"kernel": kname, "dispatches": {k: len(v) for k, v in vals.items()}, "counters": avg}
+out = {"kernel": kname, "dispatches": {k: len(v) for k, v in vals.items()}, "counters": avg,
+       # the kernel build these counters belong to (bench.py checks it before using them)
+       "kernel_sources_sha16": importlib.import_module("small-pathtracer_amd").kernel_sources_sha16()}
 if durs:
     out["avg_duration_ms"] = 1e3 * sum(durs) / len(durs)
 d = out.get("avg_duration_ms")

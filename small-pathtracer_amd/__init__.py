@@ -20,6 +20,7 @@ gfx950 device is missing — there is no CPU fallback in this package.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 from typing import Iterable, Sequence
@@ -202,7 +203,35 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         getattr(lib, name).restype = I32
     del U32
     _lib = lib
+    # spt_render's cached per-device contexts (unit slots: ~200-400 MB) are returned when the
+    # interpreter exits, not held until the process dies (a no-op when spt_render never ran)
+    atexit.register(_release_dropin_contexts)
     return lib
+
+
+# The sources the render kernel is compiled from: their hash identifies a kernel build, so a PMC
+# profile committed under profiles/ can say which kernel it measured (bench.py omits hardware-counter
+# figures whose profile was taken on other sources).
+KERNEL_SOURCES = ("csrc/spt_kernel.hip", "csrc/spt_device.h", "csrc/spt_cornell.h", "csrc/spt_diag.h",
+                  "csrc/Makefile", "../include/spt.h", "../include/spt_flops.h")
+
+
+def kernel_sources_sha16() -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(_HERE, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _release_dropin_contexts() -> None:
+    if _lib is not None:
+        try:
+            _lib.spt_shutdown()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown: nothing left to report to
+            pass
 
 
 def _check(status: int) -> None:
@@ -333,6 +362,19 @@ def spheres32_scene() -> list:
     n = ctypes.c_int32()
     _check(lib.spt_scene_spheres32(arr, 64, ctypes.byref(n)))
     return [arr[i] for i in range(n.value)]
+
+
+def move_short_box(prims: list, dx: float) -> list:
+    """rect[] of :287-311 with the short box (:305-309, prims 12-16) moved by dx along x: the HEAD
+    topology with edited geometry (the uploaded-geometry kernels; the compile-time one matches only
+    the unedited table)."""
+    out = [spt_prim.from_buffer_copy(p) for p in prims]
+    for i in (12, 13, 16):  # XY faces and the XZ top: x bounds geom[0:2]
+        out[i].geom[0] += dx
+        out[i].geom[1] += dx
+    for i in (14, 15):  # YZ faces: plane x = geom[4]
+        out[i].geom[4] += dx
+    return out
 
 
 def cornell_specular_scene() -> list:

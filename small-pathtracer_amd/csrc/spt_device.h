@@ -106,10 +106,6 @@ __device__ __forceinline__ float u16(uint32_t lo, uint32_t hi) { return (float)u
 // steps; max relative error 6e-8 / 1.3e-7 (oracle tests). rcp_nr(+-0) is NaN, which the
 // intersection treats exactly like 1/0 = inf (no hit on a parallel plane).
 __device__ __forceinline__ float rcp_nr(float x) {
-#ifdef SPT_RCP_HW  // A/B probe only (not the contract): v_rcp_f32 and one fma correction
-  const float r = __builtin_amdgcn_rcpf(x);
-  return fmaf(fmaf(-x, r, 1.0f), r, r);
-#endif
   float y = __uint_as_float(0x7EF311C3u - __float_as_uint(x));
 #pragma unroll
   for (int i = 0; i < 3; ++i) {

@@ -76,11 +76,9 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 #ifndef SPT_SCRAMBLE_K
 #define SPT_SCRAMBLE_K 8  // pixel-order spreading factor of the work units (1 = off; A/B in DESIGN.md §4)
 #endif
-#ifndef SPT_UNIT_SLOTS
-// 1: a unit's owner lane stores its three sums to the unit's own slot (plain stores, no atomics);
-// only stolen ranges add into the per-pixel accumulator; finalize_kernel sums both
-#define SPT_UNIT_SLOTS 1
-#endif
+// Unit slots: a unit's owner lane stores its three sums to the unit's own slot (plain stores, no
+// atomics); only stolen ranges add into the per-pixel accumulator; finalize_slots_kernel sums both
+// (rounds 1-2 added every unit's sums atomically)
 #ifndef SPT_STEAL_MIN
 #define SPT_STEAL_MIN 8  // unstarted samples a donor must hold (in-wave stealing; A/B in DESIGN.md §4)
 #endif
@@ -198,17 +196,9 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   int unit_dirs;  // oracle c_unit_dirs: the scene has a sphere or a REFR primitive
   float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
   unsigned long long* accum;  // [n_local_pix][3] 1.31 fixed point (stolen ranges; every unit without slots)
-  unsigned long long* slots;  // [n_units][3] one owner store per unit, unit order (SPT_UNIT_SLOTS)
-  // [0] = next unit (main launch), [16] = next leftover record (leftover launch), [32] = leftover
-  // records written (each on its own 64-byte line)
-  uint32_t* queue;
+  unsigned long long* slots;  // [n_units][3] one owner store per unit, unit order (unit slots)
+  uint32_t* queue;            // [0] = next unit
   unsigned long long* stats;  // [8]
-  // Leftover queue (two launches per frame): when a wave of the main launch first
-  // finds the unit queue dry, each of its lanes keeps the sample it is on and publishes its other
-  // unstarted samples as records of <= 2^left_sh samples (pixel, first sample, end); the leftover
-  // launch of the same kernel takes the records as its units. left_cap == 0: no records, no launch.
-  uint4* left_recs;
-  uint32_t left_cap, left_sh, left_min, sh_left;  // sh_left: guided-grab shift of the leftover launch
 };
 
 // Re-derive a wave-uniform pointer as opaque so uniform loads are re-issued (s_load) where used
@@ -352,18 +342,11 @@ constexpr uint32_t kKeyNone = __builtin_bit_cast(uint32_t, 1e20f) | 63u;  // tmi
 constexpr float kNegTiny = -0x1p-149f;
 __device__ __forceinline__ float plane_t(float n, float inv) { return fmaf(n, inv, kNegTiny); }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
-#ifndef SPT_COUNT_ADDC
-#define SPT_COUNT_ADDC 1
-#endif
 // c += b for a per-lane event counter as ONE v_addc_co_u32 with b's lane mask as its carry-in
 // (LLVM spells c + (b ? 1 : 0) as a v_cndmask and a v_add)
 __device__ __forceinline__ void count_if(uint32_t& c, bool b) {
-#if SPT_COUNT_ADDC
   const uint64_t m = __builtin_amdgcn_ballot_w64(b);
   asm("v_addc_co_u32_e64 %0, vcc, 0, %0, %1" : "+v"(c) : "s"(m) : "vcc");
-#else
-  c += b ? 1u : 0u;
-#endif
 }
 // (bits(t) | 63) ^ (63 - pos) as ONE v_bitop3 (0x36 = (S0 | S2) ^ S1)
 template <int POS>
@@ -834,19 +817,6 @@ __device__ __forceinline__ uint32_t unit_pixel(const SPT_CONST KParams* Q, uint3
   return (r & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (r >> Q->scr_k);
 }
 
-// Exclusive prefix sum over the wave (all 64 lanes active) and the wave's total.
-__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t& total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o);
-    x += lane >= (uint32_t)o ? y : 0u;
-  }
-  total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-  return x - v;
-}
-
-
 // One lane = one pixel-sample path at a time, and every iteration traces exactly ONE ray per lane
 // with the same nearest-hit loop (intersect :323-335): either the path ray toward the next vertex
 // or, after a NEE event whose light sample passes light_accepts(), the shadow ray of :466. The
@@ -860,9 +830,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uin
 // The lane state is one VGPR word (kSt*) and the small blocks are branch-free: the loop is bound
 // by instruction issue, and LLVM's exec-mask bookkeeping for loop-carried booleans and short
 // branches was SALU work on the CU's single scalar unit.
-//   PH: 0 = the main launch (units from the queue; publishes leftover records when left_cap != 0),
-//   1 = the leftover launch (units = the records the main launch published).
-template <class TP, class CF, int PH>
+template <class TP, class CF>
 // SGPRs capped at 80: with 81-96 SGPRs a CU admits only 7 blocks of 256 threads, not the 8 that the
 // compiler's occupancy report and hipOccupancyMaxActiveBlocksPerMultiprocessor() claim (MI355X_MICROARCH
 // "256-thread blocks are admitted per CU up to min(API, 8, floor(800 / (ceil(sgpr/16)*16 + 16)))";
@@ -872,10 +840,11 @@ template <class TP, class CF, int PH>
 #define SPT_NUM_SGPR 80
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(SPT_NUM_SGPR)))
-// The sphere kernels and the estimator-specialised HEAD kernels allocate for 8 waves/SIMD
+// The sphere kernels and the estimator-specialised rect kernels allocate for 8 waves/SIMD
 // explicitly: the sphere NEE kernel otherwise takes 65 VGPRs (7 waves), the HEAD NEE kernel 65 with
-// the round-2 Philox key (philox_pixel_key); with the hint both fit 64 with no spills
-__attribute__((amdgpu_waves_per_eu((TP::SPH && !TP::MAT && !TP::WIDE) || (TP::CONSTGEO && CF::NEE >= 0) ? 8 : 1)))
+// the round-2 Philox key (philox_pixel_key), the uploaded-geometry HEAD-topology ones 65; with the
+// hint all fit 64 with no spills
+__attribute__((amdgpu_waves_per_eu((TP::SPH && !TP::MAT && !TP::WIDE) || (!TP::SPH && !TP::MAT && CF::NEE >= 0) ? 8 : 1)))
 render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
@@ -891,9 +860,6 @@ render_kernel(const KParams* __restrict__ Pg) {
   if (TP::SPH && threadIdx.x < kBlock / 64) s_nsph[threadIdx.x] = 0;
   // Shadow rays resolved early, per wave, in the sphere kernels (same reason: no VGPR counter)
   __shared__ uint32_t s_nearly[TP::SPH ? kBlock / 64 : 1];
-  // Main launch: the end of the range each lane parked for the leftover launch (0: none)
-  __shared__ uint32_t s_left[PH == 0 ? kBlock : 1];
-  if (PH == 0) s_left[threadIdx.x] = 0u;
   if (TP::SPH && threadIdx.x < kBlock / 64) s_nearly[threadIdx.x] = 0;
   {
     const SPT_CONST KParams* P = cptr(Pg);
@@ -946,12 +912,6 @@ render_kernel(const KParams* __restrict__ Pg) {
               C->cam_cv[1], C->cam_l[0], C->cam_l[1], C->cam_l[2], C->fix_scale};
   }
   uint32_t pool_next = 0, pool_end = 0, grab_at = 0;  // grab_at: the wave's last queue position
-  // The leftover launch's units: the records the main launch wrote (a kernel boundary lies between)
-  uint32_t n_left = 0;
-  if constexpr (PH == 1) {
-    const SPT_CONST KParams* Q = cptr(Pg);
-    n_left = (uint32_t)__builtin_amdgcn_readfirstlane((int)min(Q->queue[32], Q->left_cap));
-  }
   bool exhausted = false, capped = false;
   // Wave-uniform event counters (SGPRs), fed by ballots at convergent points of the loop: per-lane
   // counters incremented inside the divergent blocks cost ~40 VGPRs of copies.
@@ -1008,67 +968,40 @@ render_kernel(const KParams* __restrict__ Pg) {
     while (need != 0 && !exhausted) {
       SPT_REGION(2);
       const SPT_CONST KParams* Q = cptr(Pg);
-      const uint32_t n_units = PH == 1 ? n_left : Q->n_units;
       if (pool_next >= pool_end) {
         uint32_t want = kGrab;
-        if (PH == 1 || Q->sh_guided < 32u) {
-          const uint32_t left = n_units - min(grab_at, n_units);
-          want = min(kGrab, max(max((uint32_t)__popcll(need), kGrabMin),
-                                left >> (PH == 1 ? Q->sh_left : Q->sh_guided)));
+        if (Q->sh_guided < 32u) {
+          const uint32_t left = Q->n_units - min(grab_at, (uint32_t)Q->n_units);
+          want = min(kGrab, max(max((uint32_t)__popcll(need), kGrabMin), left >> Q->sh_guided));
         }
         uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(Q->queue + (PH == 1 ? 16 : 0), want);
+        if (lane == 0) b = atomicAdd(Q->queue, want);
         b = __builtin_amdgcn_readfirstlane(b);
         grab_at = b + want;
-        if (b >= n_units) {
-          exhausted = true;
-          // The main launch's leftover: the queue is dry, so each lane keeps only
-          // the sample it is on and parks the end of its range in LDS; after the loop (where few
-          // registers are live) the rest becomes records for the leftover launch, which spreads it
-          // over the whole chip -- the young waves that the SIMD's age-first issue order starves
-          // would otherwise drain it alone. Once per wave; a lane with fewer than left_min unstarted
-          // samples keeps them.
-          if (PH == 0 && Q->left_cap != 0) {
-            const bool pub = ls != kStIdle && s_end >= s + 1u + Q->left_min;
-            s_left[threadIdx.x] = pub ? s_end : 0u;
-            s_end = pub ? s + 1u : s_end;
-          }
-          break;
-        }
+        if (b >= Q->n_units) { exhausted = true; break; }
         pool_next = b;
-        pool_end = min(b + want, n_units);
+        pool_end = min(b + want, Q->n_units);
       }
       const uint32_t rank = lane_rank(need);
       const uint32_t avail = pool_end - pool_next;
       if (needs_unit && rank < avail) {
         const uint32_t u = pool_next + rank;
-        if constexpr (PH == 1) {  // a leftover record: pixel, first sample, end (no slot: atomics)
-          const uint4 rc = Q->left_recs[u];
-          lp = rc.x;
-          s = rc.y;
-          s_end = rc.z;
-          pixel_terms(Q, lp, pk, fx, fy);
-        } else {
-          const uint32_t npix = (uint32_t)Q->n_local_pix;
-          const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major
-          lp = u - j * npix;
-          // Spread the pixel order (scr_k > 0): unit pixel lp = b * K + a -> a * (npix / K) + b, so a
-          // wave's run of consecutive units samples the whole image instead of one row segment, and
-          // per-wave work varies less (the image does not change: every pixel-sample is still done
-          // once and summed in integers)
-          lp = (lp & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (lp >> Q->scr_k);
-          s = j * (uint32_t)Q->chunk;
-          s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
-          pixel_terms(Q, lp, pk, fx, fy);
-        }
+        const uint32_t npix = (uint32_t)Q->n_local_pix;
+        const uint32_t j = div_magic(u, Q->m_npix, Q->sh_npix);  // chunk-major
+        lp = u - j * npix;
+        // Spread the pixel order (scr_k > 0): unit pixel lp = b * K + a -> a * (npix / K) + b, so a
+        // wave's run of consecutive units samples the whole image instead of one row segment, and
+        // per-wave work varies less (the image does not change: every pixel-sample is still done
+        // once and summed in integers)
+        lp = (lp & ((1u << Q->scr_k) - 1u)) * Q->scr_q + (lp >> Q->scr_k);
+        s = j * (uint32_t)Q->chunk;
+        s_end = min(s + (uint32_t)Q->chunk, (uint32_t)Q->spp);
+        pixel_terms(Q, lp, pk, fx, fy);
         if constexpr (CF::CAMAX == 1) {  // the per-pixel P_x, P_y of the camera ray (jitter_f)
           fx = fmaf(ck.aux, fx, ck.lx);
           fy = fmaf(ck.avy, fy, ck.ly);
         }
-#if SPT_UNIT_SLOTS
-        if constexpr (PH == 0)
-          lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
-#endif
+        lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
         ls = kStCam;
         needs_unit = false;
       }
@@ -1096,10 +1029,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           const uint32_t dend = (uint32_t)__builtin_amdgcn_readlane((int)s_end, dl);
           const uint32_t mid = dcur + (dend - dcur) / 2u;  // donor keeps [.., mid), taker [mid, dend)
           uint32_t d_lp = (uint32_t)__builtin_amdgcn_readlane((int)lp, dl);
-#if SPT_UNIT_SLOTS
           if (d_lp >> 31)  // an owner donor holds its unit index: the taker adds by pixel
             d_lp = unit_pixel(cptr(Pg), d_lp & 0x7FFFFFFFu);
-#endif
           const uint32_t d_qhi = (uint32_t)__builtin_amdgcn_readlane((int)pk.qhi, dl);
           const uint32_t d_qlo = (uint32_t)__builtin_amdgcn_readlane((int)pk.qlo, dl);
           const uint32_t d_lo = (uint32_t)__builtin_amdgcn_readlane((int)pk.lo, dl);
@@ -1120,23 +1051,6 @@ render_kernel(const KParams* __restrict__ Pg) {
     }
     if (__ballot(ls != kStIdle) == 0) break;
     }
-#if defined(SPT_PRIO) && SPT_PRIO > 0
-    // A/B: wave priority against the SIMD's age-first issue order ("C2")
-    if ((iter & 31u) == 0u) {
-      uint32_t pr;
-      if (SPT_PRIO == 2 || (SPT_PRIO == 3 && exhausted)) {  // tail: most remaining work first
-        const uint32_t c = (uint32_t)__popcll(__ballot(s_end >= s + 8u && ls != kStIdle));
-        pr = exhausted ? (c >= 32u ? 3u : c >= 8u ? 2u : c >= 1u ? 1u : 0u) : 0u;
-      } else {  // rotation: the wave's age rank on its SIMD plus a phase
-        pr = ((iter >> 5) + ((blockIdx.x << 3) / gridDim.x)) & 3u;
-      }
-      pr = __builtin_amdgcn_readfirstlane(pr);
-      if (pr == 0u) __builtin_amdgcn_s_setprio(0);
-      else if (pr == 1u) __builtin_amdgcn_s_setprio(1);
-      else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(3);
-    }
-#endif
     n_cos += (uint32_t)__popcll(__ballot(ls == kStCos));
 
     // 3) generate the path ray (kStCam, kStCos, kStSpec): the cosine continuation from the last
@@ -1189,10 +1103,10 @@ render_kernel(const KParams* __restrict__ Pg) {
     if (ls >= kStPath) {  // kStPath or kStShadow
       // 4) trace the lane's ray (path ray: hittingPoint :371-377; shadow ray: :466).
       SPT_REGION(4);
-#ifdef SPT_PROBE_SALU  // A/B probe: N extra SALU per wave-iteration (marginal issue cost)
+#ifdef SPT_PROBE_SALU  // diagnostic build SPT_DIAG=3: N extra SALU per wave-iteration (issue cost)
       { uint32_t z_ = iter; asm volatile(".rept " SPT_XSTR(SPT_PROBE_SALU) "\n s_add_u32 %0, %0, 1\n .endr" : "+s"(z_)); }
 #endif
-#ifdef SPT_PROBE_VALU  // A/B probe: N extra VALU per wave-iteration
+#ifdef SPT_PROBE_VALU  // diagnostic build SPT_DIAG=4: N extra VALU per wave-iteration
       { float z_ = o.x; asm volatile(".rept " SPT_XSTR(SPT_PROBE_VALU) "\n v_add_f32 %0, 1.0, %0\n .endr" : "+v"(z_)); }
 #endif
       const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
@@ -1528,15 +1442,12 @@ render_kernel(const KParams* __restrict__ Pg) {
           ls = kStCam;
           if (s >= s_end) {  // the unit's last sample: flush its pixel's fixed-point sums
             SPT_REGION(1);
-#if SPT_UNIT_SLOTS
             if (lp >> 31) {  // the unit's owner: its slot, written exactly once (zeros included)
               unsigned long long* a = cptr(Pg)->slots + 3ull * (lp & 0x7FFFFFFFu);
               a[0] = acc0;
               a[1] = acc1;
               a[2] = acc2;
-            } else
-#endif
-            {
+            } else {  // a stolen range: add into its pixel's accumulator
               unsigned long long* a = cptr(Pg)->accum + 3ull * lp;
               if (acc0) atomicAdd(a + 0, acc0);
               if (acc1) atomicAdd(a + 1, acc1);
@@ -1558,27 +1469,6 @@ render_kernel(const KParams* __restrict__ Pg) {
     reg_flags = 0;
 #endif
   }
-  if constexpr (PH == 0) {  // publish the parked ranges: every lane is idle, at s = its kept end
-    const SPT_CONST KParams* Q = cptr(Pg);
-    const uint32_t end = s_left[threadIdx.x];
-    bool lost = false;
-    if (Q->left_cap != 0 && end > s) {
-      const uint32_t piece = 1u << Q->left_sh;
-      const uint32_t nrec = (end - s + piece - 1u) >> Q->left_sh;
-      // one atomic per lane (the atomic optimizer scans them into one per wave)
-      const uint32_t base = atomicAdd(Q->queue + 32, nrec);
-      // (the host sizes left_recs for every lane's whole unit: the check never fails)
-      if (base + nrec <= Q->left_cap) {
-        const uint32_t px = (lp >> 31) ? unit_pixel(Q, lp & 0x7FFFFFFFu) : lp;
-        uint4* out = Q->left_recs + base;
-        for (uint32_t a = s, i = 0; i < nrec; ++i, a += piece)
-          out[i] = uint4{px, a, min(a + piece, end), 0u};
-      } else {
-        lost = true;  // cannot happen; if it did, report an incomplete image, never a wrong one
-      }
-    }
-    if (__ballot(lost) != 0) capped = true;
-  }
   {
     unsigned long long* st = cptr(Pg)->stats;  // wave-reduced by the atomic optimizer
 #ifdef SPT_WAVE_TIMES
@@ -1594,9 +1484,8 @@ render_kernel(const KParams* __restrict__ Pg) {
       atomicAdd(st + 18, wave_t0 >> 4);  // sums of start / end times (/16: no overflow)
       atomicAdd(st + 19, t1 >> 4);
       atomicAdd(st + 20, (unsigned long long)__smid());
-      // the leftover launch's waves from entry 16384 on (tools/wave_tail.py splits there)
-      const uint32_t wid = blockIdx.x * (kBlock / 64) + threadIdx.x / 64 + (PH == 1 ? 16384u : 0u);
-      if (wid < (PH == 1 ? 32768u : 16384u)) {
+      const uint32_t wid = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+      if (wid < 32768) {
         st[32 + 3 * wid] = wave_t0;
         st[33 + 3 * wid] = t1;
         st[34 + 3 * wid] = ((unsigned long long)__smid() << 32) | wave_iters;
@@ -1618,7 +1507,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       atomicAdd(st + 3, np);  // + the light hits, added per lane below
       atomicAdd(st + 6, (unsigned long long)n_cos);
     }
-    if (!TP::MAT && PH == 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // one camera ray per sample
+    if (!TP::MAT && blockIdx.x == 0 && threadIdx.x == 0) {  // one camera ray per sample
       const SPT_CONST KParams* C = cptr(Pg);
       const unsigned long long samples = (unsigned long long)C->n_local_pix * (unsigned long long)C->spp;
       atomicAdd(st + 1, samples);
@@ -1653,18 +1542,10 @@ render_kernel(const KParams* __restrict__ Pg) {
     }
   }
 }
-// 1.31 fixed point -> float, clamp :538 (values are >= 0 by construction).
-__global__ void __launch_bounds__(kBlock)
-finalize_kernel(const unsigned long long* __restrict__ accum, float* __restrict__ rgb, uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) {
-    const float v = (float)accum[i] * 0x1p-31f;
-    rgb[i] = v > 1.0f ? 1.0f : v;
-  }
-}
-// The same with the unit slots: thread t takes unit-order pixel t (coalesced slot reads, chunk
-// j's slot at j * npix + t), adds the pixel's stolen-range sums and writes its spread pixel
-// p = (t mod K) * (npix / K) + t / K. Integer sums: the order of the adds cannot matter.
+// 1.31 fixed point -> float, clamp :538 (values are >= 0 by construction). Thread t takes
+// unit-order pixel t (coalesced slot reads, chunk j's slot at j * npix + t), adds the pixel's
+// stolen-range sums and writes its spread pixel p = (t mod K) * (npix / K) + t / K. Integer sums:
+// the order of the adds cannot matter.
 __global__ void __launch_bounds__(kBlock)
 finalize_slots_kernel(const unsigned long long* __restrict__ accum,
                       const unsigned long long* __restrict__ slots, float* __restrict__ rgb,
@@ -1715,46 +1596,26 @@ static spt_status fail(spt_status s, const std::string& msg) {
 // level).
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
-       KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF, KV_COUNT };
-template <int PH>
-static constexpr RenderFn kRenderKernelsOf[KV_COUNT] = {
-    render_kernel<TopoGeneric, CfgRuntime, PH>, render_kernel<TopoCornell, CfgRuntime, PH>,
-    render_kernel<TopoCornellConst, CfgRuntime, PH>, render_kernel<TopoCornellConst, CfgHeadNee, PH>,
-    render_kernel<TopoCornellConst, CfgHeadCos, PH>, render_kernel<TopoSphDiff, CfgRuntime, PH>,
-    render_kernel<TopoGenericWide, CfgRuntime, PH>, render_kernel<TopoSphDiff, CfgSphNee, PH>,
-    render_kernel<TopoRectDiff, CfgRuntime, PH>, render_kernel<TopoCornellConst, CfgHeadNeeRef, PH>,
-    render_kernel<TopoCornellConst, CfgHeadCosRef, PH>, render_kernel<TopoSphDiff, CfgSphNeeRef, PH>};
-static const RenderFn* const kRenderKernels = kRenderKernelsOf<0>;     // the main launch
-static const RenderFn* const kLeftoverKernels = kRenderKernelsOf<1>;   // the leftover launch
-
-// Leftover queue settings, read once per context from the environment for A/B runs:
-// SPT_LEFTOVER=1 turns it on (A/B: it lost on C2 and C3); SPT_LEFT_PIECE = samples per
-// record (a power of two); SPT_LEFT_MIN = fewest unstarted samples a lane publishes.
-#ifndef SPT_LEFT_PIECE
-#define SPT_LEFT_PIECE 16
-#endif
-#ifndef SPT_LEFT_MIN
-#define SPT_LEFT_MIN 4
-#endif
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
-}
+       KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF,
+       KV_CORNELL_NEE, KV_CORNELL_COS, KV_COUNT };
+static const RenderFn kRenderKernels[KV_COUNT] = {
+    render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
+    render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
+    render_kernel<TopoCornellConst, CfgHeadCos>, render_kernel<TopoSphDiff, CfgRuntime>,
+    render_kernel<TopoGenericWide, CfgRuntime>, render_kernel<TopoSphDiff, CfgSphNee>,
+    render_kernel<TopoRectDiff, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNeeRef>,
+    render_kernel<TopoCornellConst, CfgHeadCosRef>, render_kernel<TopoSphDiff, CfgSphNeeRef>,
+    render_kernel<TopoCornell, CfgHeadNee>, render_kernel<TopoCornell, CfgHeadCos>};
 
 struct spt_context {
   int device = 0;
   int n_cu = 0, blocks_per_cu = 0;      // generic kernel
   int bpc[KV_COUNT] = {};               // resident blocks per CU of each variant
-  int bpc_left[KV_COUNT] = {};          // ... and of its leftover-launch form
-  bool leftover = false;                // SPT_LEFTOVER (default off)
-  uint32_t left_sh = 4, left_min = 4;   // log2 samples per record; fewest samples published
-  uint4* left_recs = nullptr;           // leftover records, grown on demand
-  size_t left_recs_cap = 0;             // records
   DevPrim* prims = nullptr;
   SceneGeo* geo = nullptr;
   unsigned long long* accum = nullptr;
   size_t accum_cap = 0;  // elements
-  unsigned long long* slots = nullptr;  // [n_units][3] (SPT_UNIT_SLOTS), grown on demand
+  unsigned long long* slots = nullptr;  // [n_units][3] unit slots, grown on demand
   size_t slots_cap = 0;                 // elements
   uint32_t* queue = nullptr;
   unsigned long long* stats = nullptr;
@@ -2120,26 +1981,16 @@ extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
             hipSuccess || bpc <= 0)
       bpc = 4;
     c->bpc[v] = bpc;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kLeftoverKernels[v], kBlock, 0) !=
-            hipSuccess || bpc <= 0)
-      bpc = 4;
-    c->bpc_left[v] = bpc;
   }
   c->blocks_per_cu = c->bpc[KV_GENERIC];
-  c->leftover = env_int("SPT_LEFTOVER", 0) != 0;
-  {
-    const int piece = std::max(1, std::min(1 << 20, env_int("SPT_LEFT_PIECE", SPT_LEFT_PIECE)));
-    uint32_t sh = 0;
-    while ((1 << (sh + 1)) <= piece) ++sh;
-    c->left_sh = sh;
-    c->left_min = (uint32_t)std::max(1, env_int("SPT_LEFT_MIN", SPT_LEFT_MIN));
-  }
+
   hipError_t e = hipMalloc(&c->prims, sizeof(DevPrim) * kMaxPrims);
   if (e == hipSuccess) e = hipMalloc(&c->geo, sizeof(SceneGeo));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_prims, sizeof(DevPrim) * kMaxPrims, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc(&c->h_geo, sizeof(SceneGeo), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(&c->d_kp, sizeof(KParams));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_kp, sizeof(KParams), hipHostMallocDefault);
+
   if (e == hipSuccess) e = hipMalloc(&c->queue, sizeof(uint32_t) * 64);
   if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(unsigned long long) * kStatWords);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -2164,9 +2015,9 @@ extern "C" spt_status spt_context_destroy(spt_context* c) {
   if (c->h_geo) (void)hipHostFree(c->h_geo);
   if (c->d_kp) (void)hipFree(c->d_kp);
   if (c->h_kp) (void)hipHostFree(c->h_kp);
+
   if (c->accum) (void)hipFree(c->accum);
   if (c->slots) (void)hipFree(c->slots);
-  if (c->left_recs) (void)hipFree(c->left_recs);
   if (c->queue) (void)hipFree(c->queue);
   if (c->stats) (void)hipFree(c->stats);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -2278,13 +2129,18 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                     p->light_dz == 36.0f && p->light_y == kRefLy && p->light_area == kRefLarea;
   K.leak_end = (p->flags & SPT_FLAG_REFERENCE_LEAKS) ? 0 : leak_end_of(prims, n_prims, g);
   // (each estimator kernel in two forms: the leak-end rule, or leaked paths as the reference's)
-  const bool head_est = cconst && kcap >= 3 && K.light_black && p->max_depth == 0 &&
-                        p->rr_depth >= 1 && cam_axis && lref;
+  const bool ref_est = K.light_black && p->max_depth == 0 && p->rr_depth >= 1 && cam_axis && lref;
+  const bool head_est = cconst && kcap >= 3 && ref_est;
+  // the HEAD topology with uploaded geometry (an edited rect[]: a box moved, a wall resized) and
+  // the reference's estimator: geometry from LDS, the estimator's branches compile-time
+  const bool cornell_est = cornell && !cconst && kcap >= 2 && ref_est && K.leak_end;
   int kv = g.n_sph_wide > 0 ? KV_WIDE : KV_GENERIC;  // (only the wide kernel has the fp64 loop)
   if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP)
     kv = K.leak_end ? KV_CONST_NEE : KV_CONST_NEE_REF;
   else if (head_est && p->nee_prob <= 0.0f) kv = K.leak_end ? KV_CONST_COS : KV_CONST_COS_REF;
   else if (cconst) kv = KV_CONST;
+  else if (cornell_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CORNELL_NEE;
+  else if (cornell_est && p->nee_prob <= 0.0f) kv = KV_CORNELL_COS;
   else if (cornell) kv = KV_CORNELL;
   else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
     kv = g.n_sph == 0 ? KV_RECTDIFF
@@ -2355,15 +2211,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     uint32_t sh = 1;  // 2^sh >= 2 x waves
     while ((1u << sh) < 2u * waves && sh < 31) ++sh;
     sh = std::min(31u, sh + (uint32_t)SPT_GUIDED_EXTRA);
-#ifndef SPT_GUIDED_ALL
-#define SPT_GUIDED_ALL 0  // A/B: guided grabs for long launches too
-#endif
-    K.sh_guided = (small_launch || SPT_GUIDED_ALL) ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
-    // the leftover launch always grabs guided (its records are few and short)
-    const uint32_t waves_l = (uint32_t)(c->n_cu * c->bpc_left[kv] * (kBlock / 64));
-    uint32_t shl = 1;
-    while ((1u << shl) < 2u * waves_l && shl < 31) ++shl;
-    K.sh_left = std::min(31u, shl + (uint32_t)SPT_GUIDED_EXTRA);
+    K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
   }
   K.chunk = chunk;
   K.steal_min = small_launch ? SPT_STEAL_MIN_SMALL : SPT_STEAL_MIN;
@@ -2402,7 +2250,6 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     lattice(K.ldzi, K.lz0, &K.lz_lattice, &K.lz_shift, &K.lz_scale, &K.lz0m1);
   }
   K.accum = c->accum;
-#if SPT_UNIT_SLOTS
   if (3ull * n_units > c->slots_cap) {  // one owner store per unit (24 B): C3 208 MB, C4/C5 ~400 MB
     if (c->slots) SPT_HIP(hipFree(c->slots));
     c->slots = nullptr;
@@ -2410,31 +2257,9 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     SPT_HIP(hipMalloc(&c->slots, 3ull * n_units * sizeof(unsigned long long)));
     c->slots_cap = 3ull * n_units;
   }
-#endif
   K.slots = c->slots;
   K.queue = c->queue;
   K.stats = c->stats;
-  // Leftover records: at most one lane's unit less its current sample per resident lane of the
-  // main launch, in records of 2^left_sh samples (C3: 524 288 lanes x 6 records x 16 B = 50 MB).
-  const int grid = c->n_cu * c->bpc[kv];
-  K.left_cap = 0;
-  K.left_sh = c->left_sh;
-  K.left_min = c->left_min;
-  if (c->leftover && (uint32_t)chunk > c->left_min) {
-    const uint64_t per_lane = ((uint64_t)chunk - 1 + (1u << c->left_sh) - 1) >> c->left_sh;
-    const uint64_t cap = (uint64_t)grid * kBlock * per_lane;
-    if (cap < 0x80000000ull) {
-      if (cap > c->left_recs_cap) {
-        if (c->left_recs) SPT_HIP(hipFree(c->left_recs));
-        c->left_recs = nullptr;
-        c->left_recs_cap = 0;
-        SPT_HIP(hipMalloc(&c->left_recs, cap * sizeof(uint4)));
-        c->left_recs_cap = cap;
-      }
-      K.left_cap = (uint32_t)cap;
-    }
-  }
-  K.left_recs = c->left_recs;
   K.light_kind = light_pos >= 0 ? prims[p->light_id].kind : 0;
   K.light_pos = light_pos;
   K.scatter_uniform = (p->flags & SPT_FLAG_UNIFORM_SCATTER) ? 1 : 0;
@@ -2452,36 +2277,26 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 
   SPT_HIP(hipMemsetAsync(c->accum, 0, sizeof(unsigned long long) * 3 * (size_t)K.n_local_pix,
                          stream));
-  SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t) * 64, stream));  // unit + leftover queues
+  SPT_HIP(hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream));
   SPT_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kStatWords, stream));
 #ifdef SPT_WAVE_TIMES
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
   c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
-                       kv == KV_SPHDIFF_NEE_REF;
+                       kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE;
+  const int grid = c->n_cu * c->bpc[kv];
   *c->h_kp = K;
   SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   SPT_HIP(hipEventRecord(c->ev0, stream));
   hipLaunchKernelGGL(kRenderKernels[kv], dim3(grid), dim3(kBlock), 0, stream,
                      (const KParams*)c->d_kp);
   SPT_HIP(hipGetLastError());
-  if (K.left_cap != 0) {  // the leftover launch: the same kernel over the published records
-    hipLaunchKernelGGL(kLeftoverKernels[kv], dim3(c->n_cu * c->bpc_left[kv]), dim3(kBlock), 0,
-                       stream, (const KParams*)c->d_kp);
-    SPT_HIP(hipGetLastError());
-  }
   SPT_HIP(hipEventRecord(c->ev1, stream));
-#if SPT_UNIT_SLOTS
   const uint32_t np = (uint32_t)K.n_local_pix;
   hipLaunchKernelGGL(finalize_slots_kernel, dim3((np + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
                      (const unsigned long long*)c->accum, (const unsigned long long*)c->slots,
                      rgb_dev, np, (uint32_t)n_chunks, K.scr_k, K.scr_q,
                      (const unsigned long long*)c->stats);
-#else
-  const uint32_t n = 3u * (uint32_t)K.n_local_pix;
-  hipLaunchKernelGGL(finalize_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
-                     (const unsigned long long*)c->accum, rgb_dev, n);
-#endif
   SPT_HIP(hipGetLastError());
   SPT_HIP(hipMemcpyAsync(c->h_stats, c->stats, sizeof(unsigned long long) * kStatWords,
                          hipMemcpyDeviceToHost, stream));
@@ -2579,6 +2394,11 @@ extern "C" spt_status spt_render(const spt_prim* prims, int32_t n_prims, const s
   spt_status st = validate(prims, n_prims, cam, p);
   if (st != SPT_OK) return st;
   if (p->device < 0 || p->device >= kMaxDropInDevices) return fail(SPT_ERR_INVALID_ARG, "bad device ordinal");
+  const size_t n = 3ull * (size_t)spt_shard_row_count(p) * (size_t)p->width;
+  if (n == 0) {  // this shard owns no rows: nothing to render, no context or device memory
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    return SPT_OK;
+  }
   DropIn& D = g_dropin[p->device];
   std::lock_guard<std::mutex> lock(D.mu);
   if (!D.ctx) {
@@ -2587,11 +2407,6 @@ extern "C" spt_status spt_render(const spt_prim* prims, int32_t n_prims, const s
       D.ctx = nullptr;
       return st;
     }
-  }
-  const size_t n = 3ull * (size_t)spt_shard_row_count(p) * (size_t)p->width;
-  if (n == 0) {  // this shard owns no rows
-    if (stats) std::memset(stats, 0, sizeof *stats);
-    return SPT_OK;
   }
   SPT_HIP(hipSetDevice(p->device));
   if (n > D.out_cap) {

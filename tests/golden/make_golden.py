@@ -119,18 +119,20 @@ def variant_pins():
         json.dump(out, f, indent=1)
 
 
-def quality_c3(ref, tmp, w=1024, h=768, spp=512, seeds=range(201, 217), k=32):
+def quality_c3(ref, tmp, w=1024, h=768, spp=512, seeds=range(201, 217), k=32, est="nee", cfg="c3"):
     """bench.py's `quality` fixture (`--quality-c3`): the reference's own C3 image (HEAD NEE,
     1024x768 @ 512 spp, the bench's config) as 32x32-block means of its linearised PPM, one set
     per independent run of oracle/_ref/smallpt_nee_xs (16 runs): ref_c3_blocks_k32.npz. The runs
     use the bench's spp because the reference clamps each PIXEL estimate to [0, 1] (:538): the
     clamp removes more of a noisier estimate, so images at different spp differ in expectation
-    (measured: 64-spp runs are 0.4 % darker than a 512-spp image)."""
+    (measured: 64-spp runs are 0.4 % darker than a 512-spp image).
+    `--quality-c2` (est "cos", cfg "c2"): the same for C2, 16 runs of smallpt_cos_xs (the cosine
+    estimator :474-477) at 1024x768 @ 64 spp: ref_c2_blocks_k32.npz."""
     from concurrent.futures import ThreadPoolExecutor
 
     def run(s):
-        path = os.path.join(tmp, f"q_{s}.ppm")
-        subprocess.run([os.path.join(ref, "smallpt_nee_xs"), str(w), str(h), str(spp), str(s), path],
+        path = os.path.join(tmp, f"q_{cfg}_{s}.ppm")
+        subprocess.run([os.path.join(ref, f"smallpt_{est}_xs"), str(w), str(h), str(spp), str(s), path],
                        check=True, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         lin = (read_ppm(path) / 255.0) ** 2.2
         os.remove(path)
@@ -138,7 +140,7 @@ def quality_c3(ref, tmp, w=1024, h=768, spp=512, seeds=range(201, 217), k=32):
 
     with ThreadPoolExecutor(max(1, (os.cpu_count() or 2) - 2)) as ex:
         blocks = np.array(list(ex.map(run, seeds)))
-    np.savez(os.path.join(HERE, f"ref_c3_blocks_k{k}.npz"), blocks=blocks, seeds=np.array(list(seeds)),
+    np.savez(os.path.join(HERE, f"ref_{cfg}_blocks_k{k}.npz"), blocks=blocks, seeds=np.array(list(seeds)),
              shape=np.array([w, h, spp, k]))
 
 
@@ -174,6 +176,13 @@ def main():
         tmp = "/tmp/spt_golden"
         os.makedirs(tmp, exist_ok=True)
         quality_c3(os.path.join(ROOT, "oracle", "_ref"), tmp)
+        return
+    if "--quality-c2" in sys.argv:
+        subprocess.run([os.path.join(ROOT, "oracle", "build_ref.sh")], check=True)
+        tmp = "/tmp/spt_golden"
+        os.makedirs(tmp, exist_ok=True)
+        quality_c3(os.path.join(ROOT, "oracle", "_ref"), tmp, spp=64, seeds=range(301, 317), est="cos",
+                   cfg="c2")
         return
     if "--variant-pins" in sys.argv:
         variant_pins()

@@ -26,7 +26,10 @@ def lines(out):
 def test_spawns_n_ranks_with_rank_environment():
     r = run(["--gpus", "3", "--probe-env"])
     assert r.returncode == 0, r.stderr
-    got = sorted(lines(r.stdout), key=lambda d: int(d["RANK"]))
+    # rank 0's JSON is the parent's stdout; the other ranks' output goes to stderr
+    (d0,) = lines(r.stdout)
+    assert d0["RANK"] == "0"
+    got = sorted(lines(r.stdout) + lines(r.stderr), key=lambda d: int(d["RANK"]))
     assert [d["RANK"] for d in got] == ["0", "1", "2"]
     assert [d["LOCAL_RANK"] for d in got] == ["0", "1", "2"]
     assert {d["WORLD_SIZE"] for d in got} == {"3"}

@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol(spt):
 
 def test_abi_version_and_status_strings(spt):
     lib = spt.load_library()
-    assert lib.spt_abi_version() == 4
+    assert lib.spt_abi_version() == 5
     for code, text in spt.STATUS.items():
         assert lib.spt_status_string(code).decode() == text
 
@@ -93,7 +93,7 @@ def test_invalid_arguments_fail_loudly(spt):
         spt.render(bad, cam, spt.default_params(width=8, height=8, spp=1))
     assert e.value.status == 1
     with pytest.raises(spt.SptError) as e:
-        spt.render(spt.cornell_scene(), cam, spt.default_params(width=8, height=8, spp=1, flags=4))
+        spt.render(spt.cornell_scene(), cam, spt.default_params(width=8, height=8, spp=1, flags=8))
     assert e.value.status == 1
 
 

@@ -36,3 +36,49 @@ def test_product_estimates_the_reference_image(spt, est, kernel):
     zg, z2 = fidelity.compare(fx[est], own)
     assert np.all(np.abs(zg) < fidelity.GLOBAL_Z_MAX), zg
     assert z2 < fidelity.BLOCK_Z2_MAX, z2
+
+
+@pytest.mark.parametrize("kernel", ["head", "generic"])
+def test_reference_leaks_estimate_the_reference_image(spt, kernel):
+    """SPT_FLAG_REFERENCE_LEAKS (leaked paths go on from the miss vertex, :371-377) estimates the
+    reference's HEAD NEE image as well: 16 seeds against the same 16 reference runs."""
+    fx = fidelity.load_fixture()
+    w, h, spp, k = fx["w"], fx["h"], fx["spp"], fx["k"]
+    own = []
+    for seed in range(1, 17):
+        kw = fidelity.params_of("nee")
+        kw["flags"] = kw.get("flags", 0) | spt.kernel_flag(kernel) | spt.FLAG_REFERENCE_LEAKS
+        p = spt.default_params(width=w, height=h, spp=spp, seed=seed, **kw)
+        own.append(fidelity.blocks(spt.render(fidelity.scene_of(spt, "nee"), spt.Camera(aspect=w / h), p), k))
+    zg, z2 = fidelity.compare(fx["nee"], own)
+    assert np.all(np.abs(zg) < fidelity.GLOBAL_Z_MAX), zg
+    assert z2 < fidelity.BLOCK_Z2_MAX, z2
+
+
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_full_size_matched_budget_quality(spt, config):
+    """The metric's quality half at the bench's own sizes: C2 (1024x768 @ 64, cosine
+    estimator) and C3 (1024x768 @ 512, NEE) -- 16 GPU renders (seeds 1-16) pooled against 16 runs of
+    the reference at the same size and spp (tests/golden/ref_c{2,3}_blocks_k32.npz), as bench.py's
+    `quality.matched_budget` computes it: the per-channel RMSE of the 32x32-block means must stay
+    within 1.15x the two pools' Monte-Carlo noise floor (an unbiased estimator reads ~1.0)."""
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_q", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cfg = bench.CONFIGS[config]
+    w, h, spp = cfg["width"], cfg["height"], cfg["spp"]
+    cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    imgs = [spt.render(spt.cornell_scene(), cam,
+                       spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"], seed=s))
+            for s in range(1, 17)]
+    q = bench.quality(imgs[0], spp, imgs[1:], config=config)
+    assert q is not None, "quality fixture missing"
+    m = q["matched_budget"]
+    assert m["gpu_runs"] == 16, m
+    assert max(m["ratio_to_floor"]) <= 1.15, m
+    if config == "c3":  # (C2's 64-spp runs have a higher floor: the ratio is the test there)
+        assert all(x < 1e-3 for x in m["rmse_vs_reference"]), m

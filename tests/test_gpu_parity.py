@@ -552,3 +552,50 @@ def test_reference_leaks_c3_rows_bit_exact(spt, oracle):
     rows = np.array([0, 191, 383, 384, 600, 767])
     cpu, _ = oracle.counter_render(spt.cornell_scene(), cam._c, p, rows=rows)
     _assert_exact(gpu[rows], cpu)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "cornell"])
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_edited_cornell_scene_bit_exact(spt, oracle, kernel, nee):
+    """rect[] edited (the short box moved 1 unit in x): the HEAD topology with uploaded geometry --
+    auto = the estimator-specialised uploaded-geometry kernels (KV_CORNELL_NEE / _COS), cornell =
+    the run-time-estimator one. Image and statistics equal the oracle's."""
+    prims = spt.move_short_box(spt.cornell_scene(), 1.0)
+    p = spt.default_params(width=64, height=48, spp=16, seed=3, nee_prob=nee,
+                           flags=spt.kernel_flag(kernel))
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    base = spt.render(spt.cornell_scene(), spt.Camera(aspect=64 / 48), p)
+    assert not np.array_equal(base, gpu)  # the edit is visible
+
+
+@pytest.mark.parametrize("side_div,size", [(16, (64, 48, 64)), (4, (40, 30, 24)), (16, (1024, 768, 512))])
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_side_launch_bit_exact(spt, oracle, side_div, size, nee):
+    """The side launch (SPT_SIDE = side_div: the last spp/side_div samples of every pixel in small
+    units, on a low-priority stream beside the main launch) renders the same image and
+    statistics as the oracle -- at C3's size on a spread subset of rows."""
+    import torch
+
+    w, h, spp = size
+    os.environ["SPT_SIDE"] = str(side_div)
+    try:
+        r = spt.Renderer(0)  # the context reads SPT_SIDE when it is created
+    finally:
+        del os.environ["SPT_SIDE"]
+    try:
+        p = spt.default_params(width=w, height=h, spp=spp, seed=5, nee_prob=nee)
+        cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+        out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+        r.render_async(spt.cornell_scene(), cam, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        gst = r.stats()
+        gpu = out.cpu().numpy()
+    finally:
+        r.close()
+    rows = np.arange(h) if h <= 48 else np.array([0, 191, 383, 384, 600, 767])
+    cpu, cst = oracle.counter_render(spt.cornell_scene(), cam._c, p, rows=rows)
+    _assert_exact(gpu[rows], cpu)
+    if h <= 48:
+        assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert gst["samples"] == w * h * spp

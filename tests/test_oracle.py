@@ -224,8 +224,10 @@ def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
     the room rule differs only for rays from outside the room (leaked paths) that pass within 2^-8
     of a wall's edge; a box slab differs from its five faces only for rays grazing an edge within
     rounding (0 of 382k random rays and 168k rays from box-face vertices, self-hits included).
-    Measured at 128x96, seed 7 (NEE): 7 of 12288 pixels differ, each by one sample's worth, path
-    rays 6789476 vs 6789479 (contract v7; v6: 6788367 vs 6788388); cosine-only: misses -0.06 %."""
+    Pinned at 128x96, seed 7 (the measured values, not loose tolerances): NEE 6 of
+    12288 pixels differ, 3.9e-7 of the image sum, path rays 6787723 vs 6787725, every other counter
+    within 4, misses 346989 vs 346968; cosine-only 1 pixel, 7.4e-7 of the sum, counters within 1,
+    misses 362143 vs 362122 (the room rule: rays from outside the room near a wall's edge)."""
     prims = oracle.scene_cornell()
     p = oracle.default_params(width=128, height=96, spp=128 if est == "nee" else 64, seed=7,
                               nee_prob=q)
@@ -238,16 +240,14 @@ def test_parallel_pairs_equal_per_rect_tests(oracle, est, q):
         oracle.set_pairs(True)
         oracle.set_leak_end(True)
     d = np.abs(a.astype(np.float64) - b)
-    # (one differing sample moves its pixel by min(L, spp) / spp: L can exceed 1 -- contract v7,
-    # NEE: 7 pixels, the largest by 4.8 / spp, 1.1e-5 of the image sum in all)
-    assert (d.max(axis=2) > 0).sum() <= 0.001 * d.shape[0] * d.shape[1]
-    assert d.sum() <= 1e-4 * a.sum()
+    max_pixels, max_frac, max_count = (6, 4e-7, 4) if est == "nee" else (1, 8e-7, 1)
+    assert (d.max(axis=2) > 0).sum() <= max_pixels
+    assert d.sum() <= max_frac * a.sum()
     assert sa["samples"] == sb["samples"]
-    for k in ("path_rays", "vertices", "nee_light_hits", "cosine_samples", "shadow_traced"):
-        # (one trapped path -- a vertex rounded into a white box bounces there until Russian
-        # roulette ends it -- is ~70 path rays: cosine-only, boxes on/off, 7023272 vs 7023342)
-        assert abs(sa[k] - sb[k]) <= 2e-5 * max(sa[k], sa["samples"]), (k, sa[k], sb[k])
-    assert abs(sa["misses"] / sb["misses"] - 1) < 2e-3, (sa["misses"], sb["misses"])
+    for k in ("path_rays", "vertices", "nee_light_hits", "cosine_samples", "shadow_traced",
+              "nee_events", "shadow_rays"):
+        assert abs(sa[k] - sb[k]) <= max_count, (k, sa[k], sb[k])
+    assert abs(sa["misses"] - sb["misses"]) <= 25, (sa["misses"], sb["misses"])
 
 
 @pytest.mark.parametrize("pairs", [True, False])
