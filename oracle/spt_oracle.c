@@ -924,6 +924,15 @@ static inline float c_plane_t(float n, float inv) {
   lo = (double)r > p ? asf(p > 0.0 ? asu(r) - 1u : asu(r) + 1u) : r;
   return (double)lo != p && p - (double)lo == (double)asf(p > 0.0 ? asu(lo) + 1u : asu(lo) - 1u) - p ? lo : r;
 }
+
+/* Test hook (round 5): the plane distance as ONE fma of the ray-constant o * inv,
+ * t = fma(k, inv, -(o * inv)), instead of (k - o) * inv -- the candidate that would take the
+ * per-plane subtraction out of the trace. 0 = the contract. */
+static int g_fused_planes = 0;
+void spt_oracle_set_fused_planes(int on) { g_fused_planes = on != 0; }
+static inline float c_pt(float k, float o, float inv) {
+  return g_fused_planes ? fmaf(k, inv, -(o * inv)) : c_plane_t(k - o, inv);
+}
 /* Test hook: how many of the n (num[i], inv[i]) give different bits from the fma form. */
 int spt_oracle_plane_t_mismatches(const float* num, const float* inv, int n) {
   int i, bad = 0;
@@ -1008,7 +1017,7 @@ static int c_light_accepts(const c_ctx* C, fv o, fv d) {
       case SPT_RECT_XZ: oa = o.y; da = d.y; break;
       default: oa = o.x; da = d.x; break;
     }
-    tt = c_plane_t(P->k - oa, spt_oracle_rcp_nr(da)); /* as inside c_intersect (contract v5) */
+    tt = c_pt(P->k, oa, spt_oracle_rcp_nr(da)); /* as inside c_intersect (contract v5) */
     switch (P->kind) {
       case SPT_RECT_XY: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.y, tt, o.y - P->mb); break;
       case SPT_RECT_XZ: a = fmaf(d.x, tt, o.x - P->ma); b = fmaf(d.z, tt, o.z - P->mb); break;
@@ -1027,7 +1036,7 @@ static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0
 static float g_proof_y0;
 static uint64_t g_proof_n, g_proof_bad;
 static int c_early_nee_proven(fv o, fv d, float* tl) {
-  const float tt = c_plane_t(81.5f - o.y, spt_oracle_rcp_nr(d.y));
+  const float tt = c_pt(81.5f, o.y, spt_oracle_rcp_nr(d.y));
   const float a = fmaf(d.x, tt, o.x - 50.0f), b = fmaf(d.z, tt, o.z - 79.5f);
   const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && c_key(tt, 8) < C_KEY_NONE;
   const int room = asu(o.x) - asu(1.0f) <= asu(99.0f) - asu(1.0f) && asu(o.z) <= asu(170.0f) &&
@@ -1116,9 +1125,9 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     }
     if (room) continue; /* below */
     {
-      const float t0 = c_plane_t(T->k0 - oa, ia);
+      const float t0 = c_pt(T->k0, oa, ia);
       if (T->id0 != T->id1) {
-        const float t1 = c_plane_t(T->k1 - oa, ia);
+        const float t1 = c_pt(T->k1, oa, ia);
         kp = c_umin(c_key(t0, T->pos0), c_key(t1, T->pos1));
         tb = asf(c_umin(asu(t0), asu(t1)));
       } else {
@@ -1141,8 +1150,8 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
     for (r = 0; r < 3; r++) {
       const c_test* T = &C->tests[C->room[r]];
       const float oa = r == 0 ? o.z : (r == 1 ? o.y : o.x), ia = r == 0 ? iz : (r == 1 ? iy : ix);
-      const int32_t k0 = (int32_t)c_key(c_plane_t(T->k0 - oa, ia), T->pos0);
-      const int32_t k1 = (int32_t)c_key(c_plane_t(T->k1 - oa, ia), T->pos1);
+      const int32_t k0 = (int32_t)c_key(c_pt(T->k0, oa, ia), T->pos0);
+      const int32_t k1 = (int32_t)c_key(c_pt(T->k1, oa, ia), T->pos1);
       en = c_imax(en, c_imin(k0, k1));
       ex = c_imin(ex, c_imax(k0, k1));
     }
@@ -1159,12 +1168,12 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   for (i = 0; i < C->n_box; i++) {
     const c_test *Z = &C->tests[C->box[i][0]], *X = &C->tests[C->box[i][1]], *Y = &C->tests[C->box[i][2]];
     const c_test* F = &C->tests[C->room[1]];
-    const int32_t kx0 = (int32_t)c_key(c_plane_t(X->k0 - o.x, ix), X->pos0);
-    const int32_t kx1 = (int32_t)c_key(c_plane_t(X->k1 - o.x, ix), X->pos1);
-    const int32_t kz0 = (int32_t)c_key(c_plane_t(Z->k0 - o.z, iz), Z->pos0);
-    const int32_t kz1 = (int32_t)c_key(c_plane_t(Z->k1 - o.z, iz), Z->pos1);
-    const int32_t ky0 = (int32_t)c_key(c_plane_t(F->k0 - o.y, iy), F->pos0);
-    const int32_t ky1 = (int32_t)c_key(c_plane_t(Y->k0 - o.y, iy), Y->pos0);
+    const int32_t kx0 = (int32_t)c_key(c_pt(X->k0, o.x, ix), X->pos0);
+    const int32_t kx1 = (int32_t)c_key(c_pt(X->k1, o.x, ix), X->pos1);
+    const int32_t kz0 = (int32_t)c_key(c_pt(Z->k0, o.z, iz), Z->pos0);
+    const int32_t kz1 = (int32_t)c_key(c_pt(Z->k1, o.z, iz), Z->pos1);
+    const int32_t ky0 = (int32_t)c_key(c_pt(F->k0, o.y, iy), F->pos0);
+    const int32_t ky1 = (int32_t)c_key(c_pt(Y->k0, o.y, iy), Y->pos0);
     const int32_t en = c_imax(c_imax(c_imin(kx0, kx1), c_imin(kz0, kz1)), c_imin(ky0, ky1));
     const int32_t ex = c_imin(c_imin(c_imax(kx0, kx1), c_imax(kz0, kz1)), c_imax(ky0, ky1));
     if (en <= ex) tmin = c_umin(tmin, c_umin((uint32_t)en, (uint32_t)ex));
@@ -1183,9 +1192,9 @@ static int c_intersect(const c_ctx* C, fv o, fv d, float* t, int* id) {
   {
     const c_prim* H = &C->prims[*id];
     switch (H->kind) {
-      case SPT_RECT_XY: *t = c_plane_t(H->k - o.z, iz); break;
-      case SPT_RECT_XZ: *t = c_plane_t(H->k - o.y, iy); break;
-      case SPT_RECT_YZ: *t = c_plane_t(H->k - o.x, ix); break;
+      case SPT_RECT_XY: *t = c_pt(H->k, o.z, iz); break;
+      case SPT_RECT_XZ: *t = c_pt(H->k, o.y, iy); break;
+      case SPT_RECT_YZ: *t = c_pt(H->k, o.x, ix); break;
       default: *t = H->wide ? c_sphere_wide(H, o, d) : c_sphere(H, o, d);
     }
   }
@@ -1221,11 +1230,12 @@ static fv c_cosine(fv nl, uint32_t ra, uint32_t rb, int uniform, int unit) {
        frame of :345-346 a signed permutation of the axes, so the direction is written out:
        nl = (sx,0,0) -> (sx*s1, sr, -sx*cr); (0,sy,0) -> (sr, sy*s1, sy*cr);
        (0,0,sz) -> (sr, -sz*cr, sz*s1). Same values as the general formula below up to the sign
-       of exact zeros. */
-    fv r;
-    if (nl.x != 0.0f) r = fv3(nl.x * s1, sr, -(nl.x * cr));
-    else if (nl.y != 0.0f) r = fv3(sr, nl.y * s1, nl.y * cr);
-    else r = fv3(sr, -(nl.z * cr), nl.z * s1);
+       of exact zeros. Round 5: written with the normal's components as 0 / +-1 weights, six fmas
+       and no compare (the kernel's cosine_vec), the values of the case-by-case form up to the sign
+       of an exact zero. */
+    const fv r = fv3(fmaf(nl.x, s1, fmaf(-fabsf(nl.x), sr, sr)),
+                     fmaf(fabsf(nl.x), sr, fmaf(nl.y, s1, -(nl.z * cr))),
+                     fmaf(nl.z, s1, (nl.y - nl.x) * cr));
     return unit ? fnormalize(r) : fnormalize_free(r);
   }
   a = fabsf(nl.x) > 0.1f ? fv3(nl.z, 0.0f, -nl.x) : fv3(0.0f, -nl.z, nl.y);

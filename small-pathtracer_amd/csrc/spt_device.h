@@ -252,13 +252,15 @@ __device__ __forceinline__ f3 cosine_vec(f3 nl, uint32_t ra, uint32_t rb, bool u
   const float cr = c * r2s, sr = s * r2s;
   // Contract: an axis-aligned normal (every rectangle's, :123,:166,:209) makes the frame of
   // :345-346 a signed permutation of the axes: (sx,0,0) -> (sx*s1, sr, -sx*cr);
-  // (0,sy,0) -> (sr, sy*s1, sy*cr); (0,0,sz) -> (sr, -sz*cr, sz*s1) (oracle c_cosine).
-  const bool ax = nl.x != 0.0f, ay = nl.y != 0.0f;
+  // (0,sy,0) -> (sr, sy*s1, sy*cr); (0,0,sz) -> (sr, -sz*cr, sz*s1) (oracle c_cosine). Written
+  // with the normal's components as 0 / +-1 weights (round 5): six fmas and no compare or select,
+  // the same values up to the sign of an exact zero, which nothing downstream reads (a zero
+  // direction component's rcp_nr is NaN for either sign).
   if (AXIS || (fabsf(nl.x) + fabsf(nl.y) + fabsf(nl.z) == 1.0f &&
                ((int)(nl.x == 0.0f) + (int)(nl.y == 0.0f) + (int)(nl.z == 0.0f)) == 2)) {
-    const float sg = ax ? nl.x : (ay ? nl.y : nl.z);
-    const float p = sg * s1, q = sg * cr;
-    return mk(ax ? p : sr, ax ? sr : (ay ? p : -q), ax ? -q : (ay ? q : p));
+    return mk(fmaf(nl.x, s1, fmaf(-fabsf(nl.x), sr, sr)),
+              fmaf(fabsf(nl.x), sr, fmaf(nl.y, s1, -(nl.z * cr))),
+              fmaf(nl.z, s1, (nl.y - nl.x) * cr));
   }
   const f3 a = fabsf(nl.x) > 0.1f ? mk(nl.z, 0.0f, -nl.x) : mk(0.0f, -nl.z, nl.y);
   const f3 u = normalize3(a);
