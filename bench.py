@@ -364,6 +364,9 @@ def main() -> None:
     ap.add_argument("--move-box", type=float, default=0.0,
                     help="edit rect[] (:287-311): move the short box by this many units in x (the "
                          "HEAD topology with uploaded geometry; 0 = the reference's table)")
+    ap.add_argument("--drop-short-box", action="store_true",
+                    help="edit rect[] (:287-311): remove the short box (:305-309), another topology "
+                         "(the uploaded-geometry rect-only kernels)")
     ap.add_argument("--reference-leaks", action="store_true",
                     help="leaked paths go on from the miss vertex as the reference's (:371-377; "
                          "SPT_FLAG_REFERENCE_LEAKS) instead of ending at their first miss (contract v6)")
@@ -448,6 +451,10 @@ def main() -> None:
     if args.move_box:
         assert cfg["scene"] == "cornell", "--move-box edits the Cornell scene"
         prims = spt.move_short_box(prims, args.move_box)
+    if args.drop_short_box:
+        assert cfg["scene"] == "cornell", "--drop-short-box edits the Cornell scene"
+        prims = spt.drop_short_box(prims)
+    edited = bool(args.move_box or args.drop_short_box)
     w, h = cfg["width"], cfg["height"]
     cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
     leak_flag = spt.FLAG_REFERENCE_LEAKS if args.reference_leaks else 0
@@ -752,8 +759,8 @@ def main() -> None:
         port = None
         if not args.no_cpu_baseline and world == 1:
             # (the reference binaries hold the unedited table: no reference leg for an edited scene)
-            cpu = None if args.move_box else reference_baseline(cfg, args.cpu_budget)
-            omp = None if args.move_box else reference_baseline(cfg, args.cpu_budget, threads=host_threads())
+            cpu = None if edited else reference_baseline(cfg, args.cpu_budget)
+            omp = None if edited else reference_baseline(cfg, args.cpu_budget, threads=host_threads())
             port = cpu_baseline(spt, prims, cam, params, img, args.cpu_budget)
             if cpu is not None and omp is not None:
                 cpu["openmp"] = omp
@@ -765,7 +772,7 @@ def main() -> None:
             spt.write_ppm(args.save_ppm, img)
         writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)
         qual = None
-        if (args.config in QUALITY_FIXTURES and world == 1 and not args.move_box
+        if (args.config in QUALITY_FIXTURES and world == 1 and not edited
                 and os.path.exists(QUALITY_FIXTURES[args.config][0])):
             # 15 more seeds of the same render (after the timed region): the matched-budget RMSE
             extra = [spt.render(prims, cam, spt.default_params(
@@ -788,6 +795,7 @@ def main() -> None:
             "config": {"workload": cfg["desc"] + (f", weak-scaled to {spp} spp over {world} GPUs"
                                                    if scaling == "weak" and world > 1 else "")
                        + (f", short box moved {args.move_box:g} in x (edited rect[])" if args.move_box else "")
+                       + (", short box removed (edited rect[])" if args.drop_short_box else "")
                        + (", leaked paths as the reference's" if args.reference_leaks else ""),
                        "width": w, "height": h, "spp": spp,
                        "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",

@@ -184,15 +184,16 @@ def counter_render_pixels(prims, cam, params, pixels, threads: int = 0):
     return out, dict(zip(_spt.STAT_KEYS, [int(v) for v in st]))
 
 
-def proof_check(on: bool, sphere_y0=None) -> None:
+def proof_check(on: bool, sphere_y0=None, edited=False) -> None:
     """Test hook: check the early shadow-ray resolve of the HEAD NEE kernel (spt_kernel.hip
     early_nee_proven) or, with sphere_y0, of the sphere NEE kernel (early_room_proven with that
-    threshold), restated as c_early_nee_proven, against c_intersect during counter renders;
-    resets the counts."""
+    threshold), or with edited=True of the uploaded-geometry HEAD-topology NEE kernel
+    (early_geo_proven, clauses by c_find_early_clauses), restated as c_early_nee_proven, against
+    c_intersect during counter renders; resets the counts."""
     L = lib()
     L.spt_oracle_proof_check.argtypes = [ctypes.c_int, ctypes.c_float]
-    L.spt_oracle_proof_check(0 if not on else (2 if sphere_y0 is not None else 1),
-                             float(sphere_y0 or 0.0))
+    mode = 0 if not on else (3 if edited else (2 if sphere_y0 is not None else 1))
+    L.spt_oracle_proof_check(mode, float(sphere_y0 or 0.0))
 
 
 def proof_counts() -> tuple:

@@ -653,6 +653,10 @@ typedef struct {
   int box[21][3];       /* their tests: XY pair (planes z), YZ pair (planes x), XZ top */
   unsigned char in_box[64]; /* test index -> 1 if it is part of a box */
   int leak_end;         /* c_find_leak_end: a path ends at its first miss */
+  /* the early-resolve clauses of an edited HEAD-topology scene (c_find_early_clauses; the host's
+     choice in spt_render_async, the kernel's early_geo_proven) */
+  float eb_top[2], eb_sgn[2], eb_bnd[2];
+  int eb_z[2];
   int unit;     /* c_unit_dirs: 1 = unit directions, 0 = the free-scale contract */
   float nee_c;  /* free-scale NEE weight constant: light_area / pi, rounded once */
 } c_ctx;
@@ -680,6 +684,7 @@ static int c_build_tests(const c_prim* P, int n, int light_id, c_test* T);
 static void c_find_room(c_ctx* C, const spt_prim* s);
 static void c_find_boxes(c_ctx* C, const spt_prim* s);
 static void c_find_leak_end(c_ctx* C, const spt_prim* s);
+static void c_find_early_clauses(c_ctx* C);
 static int g_unit_override = -1; /* test hook: -1 = the contract (c_unit_dirs), 0/1 = forced */
 void spt_oracle_set_unit_dirs(int mode) { g_unit_override = mode; }
 static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n, const spt_params* P,
@@ -700,6 +705,7 @@ static void c_ctx_init(c_ctx* C, const spt_prim* prims, const c_prim* CP, int n,
   c_find_room(C, prims);
   c_find_boxes(C, prims);
   c_find_leak_end(C, prims);
+  c_find_early_clauses(C);
   {
     int i;
     C->light_pos = -1;
@@ -1032,10 +1038,35 @@ static int c_light_accepts(const c_ctx* C, fv o, fv d) {
  * shadow ray (o, d) whose light test accepts and whose origin meets these conditions is claimed
  * to have the light as its nearest hit at the light's own t (*tl). Test-only: spt_oracle_proof_*
  * count the claims and any claim c_intersect contradicts; never changes a result. */
-static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0 - 1 in the HEAD room */
+static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0 - 1 in the HEAD room;
+                          3: an edited HEAD-topology rect[] (c_find_early_clauses) */
 static float g_proof_y0;
 static uint64_t g_proof_n, g_proof_bad;
-static int c_early_nee_proven(fv o, fv d, float* tl) {
+/* The clauses of early_geo_proven (spt_kernel.hip) for a scene with two boxes (c_find_boxes), as the
+ * host picks them from the reference's wrapped light samples (x in [31, 33), z in [62, 64)): a box
+ * with x0 >= 33 is clear for x <= x0, x1 <= 31 for x >= x1, z0 >= 64 for z <= z0, z1 <= 62 for
+ * z >= z1, any box for a vertex at or above its top (below the light plane 81.5); +inf / -inf: no
+ * clause. Whether the scene qualifies at all (the HEAD room and light) is the caller's test. */
+static void c_find_early_clauses(c_ctx* C) {
+  int b, ok = C->n_box == 2;
+  for (b = 0; b < 2; b++) {
+    C->eb_top[b] = INFINITY; C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = -INFINITY; C->eb_z[b] = 0;
+  }
+  for (b = 0; ok && b < 2; b++) {
+    const c_test *XY = &C->tests[C->box[b][0]], *YZ = &C->tests[C->box[b][1]], *T = &C->tests[C->box[b][2]];
+    const float z0 = XY->k0 < XY->k1 ? XY->k0 : XY->k1, z1 = XY->k0 < XY->k1 ? XY->k1 : XY->k0;
+    const float x0 = YZ->k0 < YZ->k1 ? YZ->k0 : YZ->k1, x1 = YZ->k0 < YZ->k1 ? YZ->k1 : YZ->k0;
+    if (!(T->k0 < 81.5f)) { ok = 0; break; }
+    C->eb_top[b] = T->k0;
+    if (x0 >= 33.0f) { C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = x0; C->eb_z[b] = 0; }
+    else if (x1 <= 31.0f) { C->eb_sgn[b] = -1.0f; C->eb_bnd[b] = -x1; C->eb_z[b] = 0; }
+    else if (z0 >= 64.0f) { C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = z0; C->eb_z[b] = 1; }
+    else if (z1 <= 62.0f) { C->eb_sgn[b] = -1.0f; C->eb_bnd[b] = -z1; C->eb_z[b] = 1; }
+  }
+  if (!ok)
+    for (b = 0; b < 2; b++) { C->eb_top[b] = INFINITY; C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = -INFINITY; }
+}
+static int c_early_nee_proven(const c_ctx* C, fv o, fv d, float* tl) {
   const float tt = c_pt(81.5f, o.y, spt_oracle_rcp_nr(d.y));
   const float a = fmaf(d.x, tt, o.x - 50.0f), b = fmaf(d.z, tt, o.z - 79.5f);
   const int acc = fabsf(a) <= 18.0f && fabsf(b) <= 16.5f && c_key(tt, 8) < C_KEY_NONE;
@@ -1047,6 +1078,14 @@ static int c_early_nee_proven(fv o, fv d, float* tl) {
   const int tall_box = o.y >= 50.0f || o.z >= 62.0f;
   *tl = tt;
   if (g_proof_on == 2) return acc && room && o.y > g_proof_y0; /* spt_kernel.hip early_room_proven */
+  if (g_proof_on == 3) { /* spt_kernel.hip early_geo_proven (an edited HEAD-topology rect[]) */
+    int b, ok = acc && room;
+    for (b = 0; b < 2; b++) {
+      const float v = C->eb_z[b] ? o.z : o.x;
+      ok = ok && (o.y >= C->eb_top[b] || v * C->eb_sgn[b] <= C->eb_bnd[b]);
+    }
+    return ok;
+  }
   return acc && room && short_box && tall_box;
 }
 void spt_oracle_proof_check(int on, float y0) {
@@ -1484,7 +1523,7 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
         sh = c_intersect(C, x, dl, &ts, &ids);
         if (g_proof_on) {
           float tl;
-          if (c_early_nee_proven(x, dl, &tl)) {
+          if (c_early_nee_proven(C, x, dl, &tl)) {
             __atomic_fetch_add(&g_proof_n, 1, __ATOMIC_RELAXED);
             if (!sh || ids != P->light_id || asu(ts) != asu(tl))
               __atomic_fetch_add(&g_proof_bad, 1, __ATOMIC_RELAXED);

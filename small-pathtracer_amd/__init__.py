@@ -377,6 +377,12 @@ def move_short_box(prims: list, dx: float) -> list:
     return out
 
 
+def drop_short_box(prims: list) -> list:
+    """rect[] of :287-311 without the short box (:305-309, prims 12-16): another topology (the
+    uploaded-geometry rect-only kernels)."""
+    return [spt_prim.from_buffer_copy(p) for p in prims[:12]]
+
+
 def cornell_specular_scene() -> list:
     """Room + light of :288-294 with smallpt's mirror (SPEC) and glass (REFR) balls (:296-297)."""
     lib = load_library()

@@ -193,6 +193,12 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // Sphere NEE kernel: vertices above early_y0 (every sphere's top + 1) in the HEAD room resolve
   // their light-accepted shadow rays early (early_room_proven); +inf when the host cannot prove it
   float early_y0;
+  // The uploaded-geometry HEAD-topology NEE kernel's early resolve (early_geo_proven): per box, a
+  // vertex at or above eb_top[b] or with sgn * x[axis] <= eb_bnd[b] (axis x, or z where eb_z[b]) has
+  // a shadow segment that cannot meet the box; eb_top = +inf and eb_bnd = -inf: no clause (the
+  // host could not prove one, or the predicate is off)
+  float eb_top[2], eb_sgn[2], eb_bnd[2];
+  uint32_t eb_z[2];
   int unit_dirs;  // oracle c_unit_dirs: the scene has a sphere or a REFR primitive
   float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
   unsigned long long* accum;  // [n_local_pix][3] 1.31 fixed point (stolen ranges; every unit without slots)
@@ -729,6 +735,22 @@ __device__ __forceinline__ bool early_room_proven(f3 x, float y0) {
 // (Round 4: the short box's "x_L < 63" is implied below y = 25: the reference's wrapped light
 // samples lie at x in [31, 33), and the crossing of y = 81.5 lies within 0.1 / (81.6 - y) < 0.0018
 // of the way back to the vertex, so x_L < 33.2 there. One compare fewer; the same predicate.)
+// The same proof for an edited rect[] of the HEAD topology (the uploaded-geometry kernels): the
+// HEAD room and light unchanged (host-checked), each box standing on the floor below the light
+// plane with a clause the host picks from the reference's wrapped light samples (x in [31, 33),
+// z in [62, 64)): a box with x0 >= 33 is clear for a vertex with x <= x0 (the segment to the light
+// stays at x <= x0) -- the HEAD short box's clause --, x1 <= 31 for x >= x1, z0 >= 64 for z <= z0,
+// z1 <= 62 for z >= z1 (the HEAD tall box's); and every box for a vertex at or above its top.
+// The oracle restates the choice (c_find_early_clauses) and checks every claim (test_oracle.py).
+__device__ __forceinline__ bool early_geo_proven(f3 x, const SPT_CONST KParams* P) {
+  int ok = early_room_ok(x);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const float v = P->eb_z[b] ? x.z : x.x;
+    ok &= (int)(x.y >= P->eb_top[b]) | (int)(v * P->eb_sgn[b] <= P->eb_bnd[b]);
+  }
+  return ok != 0;
+}
 __device__ __forceinline__ bool early_nee_proven(f3 x) {
   const int room = early_room_ok(x);
   const int short_box = (int)(x.y >= 25.0f) | (int)(x.x <= 63.0f);
@@ -930,7 +952,10 @@ render_kernel(const KParams* __restrict__ Pg) {
   // The sphere NEE kernel (C5): the same early resolve with the sphere-scene predicate.
   constexpr bool kEarlySph = !kEarlyNee && TP::SPH && !TP::MAT && !TP::WIDE && CF::NEE == 1 &&
                              CF::BLACK == 1 && CF::LREF == 1;
-  constexpr bool kEarly = kEarlyNee || kEarlySph;
+  // The uploaded-geometry HEAD-topology NEE kernel (an edited rect[]): early_geo_proven.
+  constexpr bool kEarlyGeo = !kEarlyNee && !TP::SPH && !TP::MAT && TP::NBOX == 2 && CF::NEE == 1 &&
+                             CF::BLACK == 1 && CF::LREF == 1 && CF::MAXD0 == 1;
+  constexpr bool kEarly = kEarlyNee || kEarlySph || kEarlyGeo;
   uint32_t l_early = 0;  // shadow rays resolved early (stats[kStatShadowProven])
   uint32_t l_miss = 0, l_nee = 0, l_hit = 0;
   // Shadow rays traced (NEE samples that passed light_accepts()): per lane in the rect kernels,
@@ -1354,11 +1379,12 @@ render_kernel(const KParams* __restrict__ Pg) {
               const float num = fabsf(dl.y) * adot;
               const float vv = dot3(dl, dl);
               w_nee = (num * kRefNeeC) * rcp_nr((h.tt * h.tt) * (vv * vv));
-            } else if constexpr (kEarlySph) {  // the uploaded light rect (XZ, host-checked)
+            } else if constexpr (kEarlySph || kEarlyGeo) {  // the uploaded light rect (XZ, host-checked)
               const RectHit h = rect_eval(G2->rect + D->light_pos,
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
               la = h.inb & key_valid(h.tt, (uint32_t)D->light_pos);
-              early = la & early_room_proven(x, D->early_y0);
+              if constexpr (kEarlySph) early = la & early_room_proven(x, D->early_y0);
+              else early = la & early_geo_proven(x, D);
               t = early ? h.tt : t;
             } else {
               la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
@@ -1518,7 +1544,7 @@ render_kernel(const KParams* __restrict__ Pg) {
         atomicAdd(st + 2, (unsigned long long)l_nee);
         atomicAdd(st + 4, (unsigned long long)l_nee);
       }
-      if constexpr (kEarlyNee) l_hit += l_early;  // proven shadow rays reach the light
+      if constexpr (kEarlyNee || kEarlyGeo) l_hit += l_early;  // proven shadow rays reach the light
       atomicAdd(st + 3, (unsigned long long)l_hit);
       atomicAdd(st + 5, (unsigned long long)l_hit);
       atomicAdd(st + 7, (unsigned long long)l_miss);
@@ -1529,7 +1555,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       }
       if constexpr (TP::SPH)
         if (lane == 0) atomicAdd(st + kStatSphereVertices, (unsigned long long)s_nsph[threadIdx.x / 64]);
-      if constexpr (kEarlyNee) atomicAdd(st + kStatShadowProven, (unsigned long long)l_early);
+      if constexpr (kEarlyNee || kEarlyGeo) atomicAdd(st + kStatShadowProven, (unsigned long long)l_early);
       if constexpr (kEarlySph) {
         if (lane == 0) {
           const unsigned long long ne = s_nearly[threadIdx.x / 64];
@@ -1597,7 +1623,7 @@ static spt_status fail(spt_status s, const std::string& msg) {
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
        KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF,
-       KV_CORNELL_NEE, KV_CORNELL_COS, KV_COUNT };
+       KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
@@ -1605,7 +1631,8 @@ static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGenericWide, CfgRuntime>, render_kernel<TopoSphDiff, CfgSphNee>,
     render_kernel<TopoRectDiff, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNeeRef>,
     render_kernel<TopoCornellConst, CfgHeadCosRef>, render_kernel<TopoSphDiff, CfgSphNeeRef>,
-    render_kernel<TopoCornell, CfgHeadNee>, render_kernel<TopoCornell, CfgHeadCos>};
+    render_kernel<TopoCornell, CfgHeadNee>, render_kernel<TopoCornell, CfgHeadCos>,
+    render_kernel<TopoRectDiff, CfgHeadNee>, render_kernel<TopoRectDiff, CfgHeadCos>};
 
 struct spt_context {
   int device = 0;
@@ -2143,7 +2170,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   else if (cornell_est && p->nee_prob <= 0.0f) kv = KV_CORNELL_COS;
   else if (cornell) kv = KV_CORNELL;
   else if (kv == KV_GENERIC && kcap >= 1 && all_diff && !(p->flags & SPT_FLAG_UNIFORM_SCATTER))
-    kv = g.n_sph == 0 ? KV_RECTDIFF
+    kv = g.n_sph == 0
+             // any other rect-only DIFF scene: run-time loops over the uploaded tests; with the
+             // reference's estimator its branches compile-time as well
+             ? (kcap >= 2 && ref_est && K.leak_end && p->nee_prob >= 1.0f &&
+                        p->light_mode == SPT_LIGHT_GLIBC_WRAP
+                    ? KV_RECTDIFF_NEE
+                    : kcap >= 2 && ref_est && K.leak_end && p->nee_prob <= 0.0f ? KV_RECTDIFF_COS
+                                                                                 : KV_RECTDIFF)
          : kcap >= 3 && K.light_black && lref && p->nee_prob >= 1.0f &&
                  p->light_mode == SPT_LIGHT_GLIBC_WRAP && light_pos >= 0 &&
                  prims[p->light_id].kind == SPT_RECT_XZ
@@ -2177,6 +2211,33 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
       if ((double)y0 < top + 1.0) y0 = std::nextafter(y0, INFINITY);
       K.early_y0 = y0;
     }
+  }
+  // The uploaded-geometry HEAD-topology NEE kernel's early resolve (early_geo_proven): the HEAD
+  // room and light (prims 0..6 bit-equal to :288-294) and two boxes below the light plane; per box
+  // the clause the reference's wrapped light samples allow (oracle c_find_early_clauses). Anything
+  // else: no clause, nothing resolved early.
+  for (int b = 0; b < 2; ++b) {
+    K.eb_top[b] = INFINITY; K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = -INFINITY; K.eb_z[b] = 0;
+  }
+  if (kv == KV_CORNELL_NEE && g.n_box == 2 && n_prims >= 7) {
+    spt_prim head[17];
+    int32_t nh = 0;
+    bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
+    for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
+    const int nt = g.n_txy + g.n_txz + g.n_tyz;
+    for (int b = 0; ok && b < 2; ++b) {
+      const GeoTest &XY = g.test[nt + 3 + 3 * b], &YZ = g.test[nt + 4 + 3 * b], &T = g.test[nt + 5 + 3 * b];
+      const float z0 = std::min(XY.k0, XY.k1), z1 = std::max(XY.k0, XY.k1);
+      const float x0 = std::min(YZ.k0, YZ.k1), x1 = std::max(YZ.k0, YZ.k1);
+      if (!(T.k0 < 81.5f)) { ok = false; break; }
+      K.eb_top[b] = T.k0;
+      if (x0 >= 33.0f) { K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = x0; K.eb_z[b] = 0; }
+      else if (x1 <= 31.0f) { K.eb_sgn[b] = -1.0f; K.eb_bnd[b] = -x1; K.eb_z[b] = 0; }
+      else if (z0 >= 64.0f) { K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = z0; K.eb_z[b] = 1; }
+      else if (z1 <= 62.0f) { K.eb_sgn[b] = -1.0f; K.eb_bnd[b] = -z1; K.eb_z[b] = 1; }
+    }
+    if (!ok)
+      for (int b = 0; b < 2; ++b) { K.eb_top[b] = INFINITY; K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = -INFINITY; }
   }
   // Unit size: SPT_UNITS_PER_LANE (8) units per resident lane (C3: 96 samples); never changes
   // results (integer accumulation). Round 1 chose 16 (25.0 ms vs 26.0 ms at 8 units/lane, before
@@ -2283,7 +2344,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
   c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
-                       kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE;
+                       kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE || kv == KV_RECTDIFF_NEE;
   const int grid = c->n_cu * c->bpc[kv];
   *c->h_kp = K;
   SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));

@@ -554,6 +554,19 @@ def test_reference_leaks_c3_rows_bit_exact(spt, oracle):
     _assert_exact(gpu[rows], cpu)
 
 
+@pytest.mark.parametrize("kernel", ["auto", "generic"])
+@pytest.mark.parametrize("nee", [1.0, 0.0])
+def test_other_topology_rect_scene_bit_exact(spt, oracle, kernel, nee):
+    """rect[] without the short box (another topology): auto = the estimator-specialised rect-only
+    kernels (KV_RECTDIFF_NEE / _COS), generic = the generic kernel. Equal to the oracle."""
+    prims = spt.drop_short_box(spt.cornell_scene())
+    p = spt.default_params(width=64, height=48, spp=16, seed=4, nee_prob=nee,
+                           flags=spt.kernel_flag(kernel))
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
 @pytest.mark.parametrize("kernel", ["auto", "cornell"])
 @pytest.mark.parametrize("nee", [1.0, 0.0])
 def test_edited_cornell_scene_bit_exact(spt, oracle, kernel, nee):
@@ -599,3 +612,24 @@ def test_side_launch_bit_exact(spt, oracle, side_div, size, nee):
     if h <= 48:
         assert {k: gst[k] for k in spt.STAT_KEYS} == cst
     assert gst["samples"] == w * h * spp
+
+
+@pytest.mark.parametrize("edit", range(5))
+def test_edited_scene_early_resolve_matches_oracle_proof(spt, oracle, edit):
+    """An edited rect[] of the HEAD topology (boxes moved: every clause of early_geo_proven occurs)
+    on the uploaded-geometry NEE kernel: image and statistics bit-exact, and the shadow rays it
+    resolved without a trace are exactly the oracle's claims, none contradicted."""
+    import test_oracle as to
+
+    prims = to._move_boxes(spt, **to.EDITS[edit])
+    p = spt.default_params(width=96, height=72, spp=16, seed=2 + edit)
+    oracle.proof_check(True, edited=True)
+    try:
+        gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert bad == 0 and claims > 0, (claims, bad)
+    assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)

@@ -469,3 +469,39 @@ def test_leaked_paths_end_at_their_first_miss(oracle, nee):
         assert np.array_equal(a, b)
     assert sa["misses"] < sb["misses"] and sa["vertices"] < 0.98 * sb["vertices"]
     assert sa["samples"] == sb["samples"]
+
+
+def _move_boxes(spt, short=(0.0, 0.0), tall=(0.0, 0.0)):
+    """rect[] with the short box (prims 12-16) and the tall box (7-11) moved by (dx, dz)."""
+    prims = [spt.spt_prim.from_buffer_copy(p) for p in spt.cornell_scene()]
+    for base, (dx, dz) in ((12, short), (7, tall)):
+        for i in (base, base + 1):       # XY faces: x bounds geom[0:2], plane z = geom[4]
+            prims[i].geom[0] += dx; prims[i].geom[1] += dx; prims[i].geom[4] += dz
+        for i in (base + 2, base + 3):   # YZ faces: z bounds geom[2:4], plane x = geom[4]
+            prims[i].geom[2] += dz; prims[i].geom[3] += dz; prims[i].geom[4] += dx
+        t = prims[base + 4]              # XZ top: x bounds geom[0:2], z bounds geom[2:4]
+        t.geom[0] += dx; t.geom[1] += dx; t.geom[2] += dz; t.geom[3] += dz
+    return prims
+
+
+EDITS = [dict(short=(1.0, 0.0)), dict(short=(-20.0, 0.0)), dict(short=(-35.0, 0.0)),
+         dict(short=(0.0, 30.0), tall=(40.0, -10.0)), dict(tall=(-5.0, 60.0))]
+
+
+@pytest.mark.parametrize("edit", range(len(EDITS)))
+def test_early_nee_resolve_proof_holds_edited_geometry(oracle, spt, edit):
+    """The uploaded-geometry HEAD-topology NEE kernel's early resolve (early_geo_proven, clauses by
+    c_find_early_clauses from each box's position relative to the reference's wrapped light
+    samples) against the contract's intersect on edited rect[]s -- boxes moved so that every
+    clause (x <= x0, x >= x1, z <= z0, z >= z1, top only) occurs: no claim contradicted."""
+    prims = _move_boxes(spt, **EDITS[edit])
+    p = oracle.default_params(width=128, height=96, spp=32, seed=7)
+    assert oracle.scene_boxes(prims, p) == 2
+    oracle.proof_check(True, edited=True)
+    try:
+        _, st = oracle.counter_render(prims, oracle.camera(128 / 96), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    assert bad == 0, (claims, bad)
+    assert claims > 0.3 * st["nee_light_hits"], (claims, st["nee_light_hits"])
