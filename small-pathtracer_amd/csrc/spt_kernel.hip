@@ -69,6 +69,9 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 #ifndef SPT_SMALL_UNITS
 #define SPT_SMALL_UNITS 1.5
 #endif
+#ifndef SPT_SMALL_BPC
+#define SPT_SMALL_BPC 4  // resident blocks per CU of a short launch (host, spt_render_async)
+#endif
 // Units per resident lane of a long launch (host, spt_render_async): 8 since round 4 (was 16)
 #ifndef SPT_UNITS_PER_LANE
 #define SPT_UNITS_PER_LANE 8.0
@@ -2246,10 +2249,17 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // Gsamples/s at 48 / 64 / 80 / 96 / 112 samples per unit, isolated kernel 11.67 / 11.60 / 11.60 /
   // 11.68 / 11.70 ms -- fewer refills and retires, and the next frame fills the longer tail.
   int chunk = p->chunk;
-  const double lanes = (double)c->n_cu * c->bpc[kv] * kBlock;  // resident lanes of THIS kernel
   const double rays_per_sample = p->nee_prob > 0.0f ? 5.3 : 8.9;  // HEAD: NEE / cosine only
-  const double lane_iters = (double)K.n_local_pix * p->spp * rays_per_sample / lanes;
+  const double lane_iters = (double)K.n_local_pix * p->spp * rays_per_sample /
+                            ((double)c->n_cu * c->bpc[kv] * kBlock);
   const bool small_launch = lane_iters < SPT_SMALL_ITERS;
+  // A short launch takes at most SPT_SMALL_BPC blocks per CU (half the chip's wave slots): its tail
+  // is most of it, and the frame behind it (frames in flight) then runs beside it on the other half
+  // instead of only in its tail. C2, round 5 (profiles/r05_blocks_per_cu_ab.json, 4 rounds): bench
+  // value 17.9-18.8 -> 21.4-22.1 Gsamples/s, isolated kernel 2.88-2.95 -> 2.84-2.88 ms. Long launches
+  // keep every slot (C3 at 4 blocks: isolated +8 %, value within 1 %).
+  const int bpc = small_launch ? std::min(c->bpc[kv], SPT_SMALL_BPC) : c->bpc[kv];
+  const double lanes = (double)c->n_cu * bpc * kBlock;  // resident lanes of THIS launch
   if (chunk <= 0) {
     if (small_launch) {
       // A short launch (C2: ~860 lane-iterations per lane): deal ~SPT_SMALL_UNITS units per lane
@@ -2268,7 +2278,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     chunk = std::min(chunk, p->spp);
   }
   {
-    const uint32_t waves = (uint32_t)(c->n_cu * c->bpc[kv] * (kBlock / 64));
+    const uint32_t waves = (uint32_t)(c->n_cu * bpc * (kBlock / 64));
     uint32_t sh = 1;  // 2^sh >= 2 x waves
     while ((1u << sh) < 2u * waves && sh < 31) ++sh;
     sh = std::min(31u, sh + (uint32_t)SPT_GUIDED_EXTRA);
@@ -2345,7 +2355,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 #endif
   c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
                        kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE || kv == KV_RECTDIFF_NEE;
-  const int grid = c->n_cu * c->bpc[kv];
+  const int grid = c->n_cu * bpc;
   *c->h_kp = K;
   SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
   SPT_HIP(hipEventRecord(c->ev0, stream));
