@@ -46,10 +46,14 @@ def classify(op):
 
 def blocks_of(path, key, bb=False):
     lines = open(path).read().splitlines()
+    # mangled kernels by a substring of the name, extern "C" ones by the whole name ("k_philox:")
     start = next(i for i, l in enumerate(lines)
-                 if l.startswith("_Z") and key in l and ":" in l and not l.startswith("\t"))
+                 if (l.startswith("_Z") and key in l and ":" in l and not l.startswith("\t"))
+                 or l.startswith(key))
     blocks, cur = [], None
-    for l in lines[start:]:
+    for n, l in enumerate(lines[start:]):
+        if n == 0 and not l.startswith("_Z"):
+            l = "_Z" + l  # an extern "C" entry label starts the first block like a mangled one
         s = l.strip()
         if s == "s_endpgm":
             break
