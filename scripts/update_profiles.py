@@ -34,7 +34,8 @@ json.dump({
     "hbm_bytes_per_launch": fetch + write,
     "kernel_sources_sha16": summ["kernel_sources_sha16"],
     "note": "writes are the unit slots (one 24-byte owner store of three 64-bit fixed-point sums per "
-            "work unit, 8.39 M units at C3 = 201 MB) plus the 64-bit atomics of the ranges stolen "
-            "in the tail",
+            "work unit; C3 since round 4: 96-sample units, 6 passes x 786,432 pixels = 4.72 M units "
+            "= 113 MB) plus the 64-bit atomics of the ranges stolen in the tail (three per range, "
+            "each a whole-sector write)",
 }, open(os.path.join(prof, "traffic_c3.json"), "w"), indent=1)
 print("kernel avg ms", summ["avg_duration_ms"], "hbm bytes/launch", fetch + write)
