@@ -76,6 +76,18 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 #ifndef SPT_UNITS_PER_LANE
 #define SPT_UNITS_PER_LANE 8.0
 #endif
+// Young blocks of a long launch (host, spt_render_async): the waves of the blocks a CU received
+// last (blockIdx >= SPT_YOUNG_RANK x n_cu at 8 blocks per CU) take no new pool once SPT_YOUNG_CUT per
+// mille of the units are handed out. The SIMD issues oldest-first, so these waves get the fewest
+// slots (C3: the two youngest of a CU's 8 blocks do ~4 % of the work) and the units they hold end
+// the launch. Round 5 A/B (profiles/r05_young_cut_ab.json): C3 isolated kernel -1.3 to -1.6 %,
+// C4 -0.8 %, values flat; the sphere kernels (C5 +3.6 %) keep every block grabbing.
+#ifndef SPT_YOUNG_CUT
+#define SPT_YOUNG_CUT 300
+#endif
+#ifndef SPT_YOUNG_RANK
+#define SPT_YOUNG_RANK 6
+#endif
 #ifndef SPT_SCRAMBLE_K
 #define SPT_SCRAMBLE_K 8  // pixel-order spreading factor of the work units (1 = off; A/B in DESIGN.md §4)
 #endif
@@ -176,6 +188,9 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // lanes need, kGrabMin, left >> sh_guided)) units per queue atomic, left = units not yet handed
   // out, so no wave hoards a full pool while the queue runs dry. sh_guided = 32: always kGrab.
   uint32_t sh_guided;
+  // young blocks (SPT_YOUNG_CUT): blockIdx >= young_block take no new pool once the queue is at
+  // young_cut; young_block = UINT32_MAX: off
+  uint32_t young_block, young_cut;
   uint32_t scr_k, scr_q;  // pixel-order spreading of the units: K = 2^scr_k, scr_q = npix / K
   float inv_spp, inv_w, inv_h;
   float fix_scale;  // inv_spp * 2^31 (fix31)
@@ -1001,6 +1016,14 @@ render_kernel(const KParams* __restrict__ Pg) {
         if (Q->sh_guided < 32u) {
           const uint32_t left = Q->n_units - min(grab_at, (uint32_t)Q->n_units);
           want = min(kGrab, max(max((uint32_t)__popcll(need), kGrabMin), left >> Q->sh_guided));
+        }
+        // a young block's wave (SPT_YOUNG_CUT) past the cut takes no new pool: its lanes finish and
+        // split what they hold (in-wave stealing) and the wave leaves
+        if (blockIdx.x >= Q->young_block) {
+          uint32_t q = 0;
+          if (lane == 0) q = __hip_atomic_load(Q->queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          q = __builtin_amdgcn_readfirstlane(q);
+          if (q >= Q->young_cut) { exhausted = true; break; }
         }
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(Q->queue, want);
@@ -2285,11 +2308,18 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     K.sh_guided = small_launch ? sh : 32u;  // guided grabs cost C3 ~1 % (A/B), help C2
   }
   K.chunk = chunk;
+  K.young_block = 0xFFFFFFFFu;
+  K.young_cut = 0xFFFFFFFFu;
   K.steal_min = small_launch ? SPT_STEAL_MIN_SMALL : SPT_STEAL_MIN;
   const uint64_t n_chunks = ((uint64_t)p->spp + chunk - 1) / chunk;
   const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
   if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
+  // rect-only scenes at 8 blocks per CU (the measured shape; the sphere kernels' C5 lost 3.6 %)
+  if (!small_launch && bpc == 8 && g.n_sph == 0 && SPT_YOUNG_CUT > 0) {
+    K.young_block = (uint32_t)(SPT_YOUNG_RANK * c->n_cu);
+    K.young_cut = (uint32_t)(n_units * (uint64_t)SPT_YOUNG_CUT / 1000u);
+  }
   magic31((uint32_t)K.n_local_pix, &K.m_npix, &K.sh_npix);
   // pixel-order spreading: the largest K = 2^k <= SPT_SCRAMBLE_K dividing n_local_pix
   K.scr_k = 0;
