@@ -81,7 +81,7 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 // mille of the units are handed out. The SIMD issues oldest-first, so these waves get the fewest
 // slots (C3: the two youngest of a CU's 8 blocks do ~4 % of the work) and the units they hold end
 // the launch. Round 5 A/B (profiles/r05_young_cut_ab.json): C3 isolated kernel -1.3 to -1.6 %,
-// C4 -0.8 %, values flat; the sphere kernels (C5 +3.6 %) keep every block grabbing.
+// C4 -0.8 %, values flat; applied to the literal HEAD NEE kernels only (the others lost).
 #ifndef SPT_YOUNG_CUT
 #define SPT_YOUNG_CUT 300
 #endif
@@ -2315,8 +2315,10 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
   if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
-  // rect-only scenes at 8 blocks per CU (the measured shape; the sphere kernels' C5 lost 3.6 %)
-  if (!small_launch && bpc == 8 && g.n_sph == 0 && SPT_YOUNG_CUT > 0) {
+  // the literal HEAD NEE kernels at 8 blocks per CU only (the measured shape): the sphere kernel
+  // (C5) lost 3.6 %, the uploaded-geometry and edited-scene kernels 0.5-2.4 % of kernel time or
+  // ~1.5 % of pipelined value (profiles/r05_young_cut_ab.json)
+  if (!small_launch && bpc == 8 && (kv == KV_CONST_NEE || kv == KV_CONST_NEE_REF) && SPT_YOUNG_CUT > 0) {
     K.young_block = (uint32_t)(SPT_YOUNG_RANK * c->n_cu);
     K.young_cut = (uint32_t)(n_units * (uint64_t)SPT_YOUNG_CUT / 1000u);
   }
