@@ -583,35 +583,23 @@ def test_edited_cornell_scene_bit_exact(spt, oracle, kernel, nee):
     assert not np.array_equal(base, gpu)  # the edit is visible
 
 
-@pytest.mark.parametrize("side_div,size", [(16, (64, 48, 64)), (4, (40, 30, 24)), (16, (1024, 768, 512))])
-@pytest.mark.parametrize("nee", [1.0, 0.0])
-def test_side_launch_bit_exact(spt, oracle, side_div, size, nee):
-    """The side launch (SPT_SIDE = side_div: the last spp/side_div samples of every pixel in small
-    units, on a low-priority stream beside the main launch) renders the same image and
-    statistics as the oracle -- at C3's size on a spread subset of rows."""
-    import torch
-
-    w, h, spp = size
-    os.environ["SPT_SIDE"] = str(side_div)
-    try:
-        r = spt.Renderer(0)  # the context reads SPT_SIDE when it is created
-    finally:
-        del os.environ["SPT_SIDE"]
-    try:
-        p = spt.default_params(width=w, height=h, spp=spp, seed=5, nee_prob=nee)
-        cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
-        out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
-        r.render_async(spt.cornell_scene(), cam, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        gst = r.stats()
-        gpu = out.cpu().numpy()
-    finally:
-        r.close()
-    rows = np.arange(h) if h <= 48 else np.array([0, 191, 383, 384, 600, 767])
-    cpu, cst = oracle.counter_render(spt.cornell_scene(), cam._c, p, rows=rows)
-    _assert_exact(gpu[rows], cpu)
-    if h <= 48:
-        assert {k: gst[k] for k in spt.STAT_KEYS} == cst
-    assert gst["samples"] == w * h * spp
+@pytest.mark.parametrize("flags", [0, 4])
+def test_full_size_scheduling_never_changes_results(spt, flags):
+    """At C3's full size the launch is long, so the young-block cut (SPT_YOUNG_CUT)
+    is active: the two youngest blocks of each CU stop taking work after 30 % of the units. Units of
+    another size hand different samples to different lanes and blocks, and the image and every
+    path statistic must stay identical (integer accumulation, counter RNG). flags 4: the reference's
+    leaks (SPT_FLAG_REFERENCE_LEAKS, the other kernel the cut applies to)."""
+    w, h, spp = 1024, 768, 512
+    cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    runs = []
+    for chunk in (0, 64):
+        p = spt.default_params(width=w, height=h, spp=spp, seed=7, flags=flags, chunk=chunk)
+        runs.append(spt.render(spt.cornell_scene(), cam, p, return_stats=True))
+    (a, sa), (b, sb) = runs
+    assert np.array_equal(a, b)
+    assert {k: sa[k] for k in spt.STAT_KEYS} == {k: sb[k] for k in spt.STAT_KEYS}
+    assert sa["samples"] == w * h * spp
 
 
 @pytest.mark.parametrize("edit", range(5))
