@@ -405,8 +405,8 @@ def test_contract_path_statistics_match_reference(oracle, nee):
 # seeds cost ~10 CPU-minutes, and sph16 pins the same fp32 sphere test here.
 @pytest.mark.parametrize("est", ["nee", "cos", "uni", "q05", "sph16"])
 def test_contract_fidelity_vs_reference_runs(oracle, spt, est):
-    """P2 for the contract itself (the CPU statement the GPU is bit-exact with): 4 seeds at
-    256x192@256 against 16 independent runs of the reference binary (tests/fidelity.py).
+    """P2 for the contract itself (the CPU statement the GPU is bit-exact with): 4 seeds (sph16: 2)
+    at 256x192@256 against 16 independent runs of the reference binary (tests/fidelity.py).
     sph16: the 32-sphere scene of config 5 (depth cap 16), whose fp32 sphere test (eps 2e-3) is
     pinned here against the reference's own fp64 Sphere::intersect (eps 1e-4, :229-239)."""
     import fidelity
@@ -414,7 +414,9 @@ def test_contract_fidelity_vs_reference_runs(oracle, spt, est):
     w, h, spp, k = fx["w"], fx["h"], fx["spp"], fx["k"]
     prims = fidelity.scene_of(spt, est)
     own = []
-    for seed in (1, 2, 3, 4):
+    # sph16 with 2 seeds: its depth-16 sphere paths cost the CPU suite ~2 minutes at 4; the GPU P2
+    # test (tests/test_gpu_fidelity.py) runs the same contract with 16 seeds, bit-exact with this one
+    for seed in ((1, 2) if est == "sph16" else (1, 2, 3, 4)):
         p = oracle.default_params(width=w, height=h, spp=spp, seed=seed, **fidelity.params_of(est))
         img, _ = oracle.counter_render(prims, oracle.camera(w / h), p)
         own.append(fidelity.blocks(img, k))
