@@ -249,9 +249,13 @@ struct CornellRectPtr {
 // NT*: rect tests per kind (parallel pairs count once).
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false,
           int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_, bool WIDE_ = false,
-          int NBOX_ = -1>
+          int NBOX_ = -1, bool UPBOX_ = false>
 struct Topo {
   static constexpr int NBOX = NBOX_;  // boxes of contract v6 (uploaded geometry; -1 = run time)
+  // CONSTGEO with the two boxes uploaded (an edited rect[] whose room and light are HEAD's): the
+  // room and light as literals, the boxes' slab tests from LDS, the early resolve's box clauses
+  // from KParams (early_geo_proven)
+  static constexpr bool UPBOX = UPBOX_;
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
   static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
@@ -265,6 +269,9 @@ struct Topo {
 // pairs; light + 2 box tops; 2 YZ box pairs
 using TopoCornell = Topo<6, 5, 6, false, 8, false, 0, 1, 0, false, false, 2>;
 using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true>;
+// the same with the boxes uploaded (a box moved or resized; room, light and topology HEAD's)
+using TopoCornellUpBox = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true, -1, -1,
+                              -1, false, false, 2, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 // Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
 // no SPEC/REFR stack and branch words, 8 waves/SIMD instead of the generic kernel's 6.
@@ -581,7 +588,7 @@ __device__ __forceinline__ int n_of(int ct, int rt) { return ct >= 0 ? ct : rt; 
 template <class TP>
 __device__ __forceinline__ auto tests_of(const SPT_CONST SceneGeo* G, const GeoTest* lds) {
   constexpr bool kLds = !TP::WIDE;
-  if constexpr (TP::CONSTGEO) {
+  if constexpr (TP::CONSTGEO && !TP::UPBOX) {
     (void)G; (void)lds;
     return (const SPT_CONST GeoTest*)nullptr;  // the HEAD tests are literals (kCornellTests)
   } else if constexpr (kLds) {
@@ -607,7 +614,14 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
                           ray6<2>(o, d, ix, iy, iz)};
     cornell_room(rays, tmin);
     cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);
-    cornell_boxes(std::make_integer_sequence<int, kCornellBoxes.n>{}, rays, tmin);
+    if constexpr (TP::UPBOX) {
+      // the uploaded HEAD-topology tests (host-checked: n_txy 0, n_txz 1, n_tyz 0): the light, the
+      // room's three pairs (its XZ pair's k0 the floor), then the two boxes' three tests each
+      geo_box(tests + 4, tests + 2, rays[2], rays[1], rays[0], tmin);
+      geo_box(tests + 7, tests + 2, rays[2], rays[1], rays[0], tmin);
+    } else {
+      cornell_boxes(std::make_integer_sequence<int, kCornellBoxes.n>{}, rays, tmin);
+    }
   } else {
     const int ntxy = n_of<TP>(TP::NTXY, G->n_txy), ntxz = n_of<TP>(TP::NTXZ, G->n_txz);
     const int ntyz = n_of<TP>(TP::NTYZ, G->n_tyz);
@@ -888,7 +902,7 @@ __attribute__((amdgpu_waves_per_eu((TP::SPH && !TP::MAT && !TP::WIDE) || (!TP::S
 render_kernel(const KParams* __restrict__ Pg) {
   __shared__ DevPrim s_prims[kMaxPrims];
   __shared__ int s_pos2idx[kMaxPrims];  // grouped position -> primitive index
-  __shared__ GeoTest s_test[TP::CONSTGEO || TP::WIDE ? 1 : kMaxPrims];
+  __shared__ GeoTest s_test[(TP::CONSTGEO && !TP::UPBOX) || TP::WIDE ? 1 : kMaxPrims];
   // Pending REFR refraction children (:494-495 at depth <= 2), two per lane at most (MAT only):
   // o, d, T, depth, branch.
   struct Node { float o[3], d[3], T[3]; int depth; uint32_t branch; };
@@ -909,7 +923,7 @@ render_kernel(const KParams* __restrict__ Pg) {
       // HEAD geometry (every primitive a rectangle): s_prims by grouped position (kPosIds)
       s_prims[i] = P->prims[TP::CONSTGEO ? G->rect[i].idx : i];
       s_pos2idx[i] = i < nrect ? G->rect[i].idx : G->sph[i - nrect].idx;
-      if (!TP::CONSTGEO && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz + 3 * G->has_room + 3 * G->n_box) {
+      if ((!TP::CONSTGEO || TP::UPBOX) && !TP::WIDE && i < G->n_txy + G->n_txz + G->n_tyz + 3 * G->has_room + 3 * G->n_box) {
         const SPT_CONST GeoTest& q = G->test[i];
         s_test[i] = GeoTest{q.k0, q.k1, q.ma, q.ha, q.mb, q.hb, q.pos0, q.pos1};
       }
@@ -1396,7 +1410,8 @@ render_kernel(const KParams* __restrict__ Pg) {
               const RectHit h = rect_eval(CornellRectPtr{kCornellLightPos},
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
               la = h.inb & key_valid(h.tt, kCornellLightPos);
-              early = la & early_nee_proven(x);
+              if constexpr (TP::UPBOX) early = la & early_geo_proven(x, D);
+              else early = la & early_nee_proven(x);
               // The weight of :471-472 now, for a proven lane and a traced one alike: nee_weight's
               // arithmetic with |dl . nl| = |dl_a| on the normal's axis a (the dot's zero terms are
               // exact) and t = the light's own t, the bits the trace returns for it. The resolve
@@ -1649,7 +1664,7 @@ static spt_status fail(spt_status s, const std::string& msg) {
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
        KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF,
-       KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_COUNT };
+       KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_UPBOX_NEE, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
@@ -1658,7 +1673,8 @@ static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoRectDiff, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNeeRef>,
     render_kernel<TopoCornellConst, CfgHeadCosRef>, render_kernel<TopoSphDiff, CfgSphNeeRef>,
     render_kernel<TopoCornell, CfgHeadNee>, render_kernel<TopoCornell, CfgHeadCos>,
-    render_kernel<TopoRectDiff, CfgHeadNee>, render_kernel<TopoRectDiff, CfgHeadCos>};
+    render_kernel<TopoRectDiff, CfgHeadNee>, render_kernel<TopoRectDiff, CfgHeadCos>,
+    render_kernel<TopoCornellUpBox, CfgHeadNee>};
 
 struct spt_context {
   int device = 0;
@@ -2250,6 +2266,9 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
     int32_t nh = 0;
     bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
     for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
+    // the room and light are HEAD's: at the auto level the boxes-only-uploaded kernel (the room,
+    // the light and the estimator literal); the const level keeps the uploaded-geometry kernel
+    if (ok && kcap >= 3) kv = KV_UPBOX_NEE;
     const int nt = g.n_txy + g.n_txz + g.n_tyz;
     for (int b = 0; ok && b < 2; ++b) {
       const GeoTest &XY = g.test[nt + 3 + 3 * b], &YZ = g.test[nt + 4 + 3 * b], &T = g.test[nt + 5 + 3 * b];
@@ -2315,10 +2334,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   const uint64_t n_units = n_chunks * (uint64_t)K.n_local_pix;
   if (n_units >= 0x80000000ull) return fail(SPT_ERR_INVALID_ARG, "too many work units; raise chunk");
   K.n_units = (uint32_t)n_units;
-  // the literal HEAD NEE kernels at 8 blocks per CU only (the measured shape): the sphere kernel
-  // (C5) lost 3.6 %, the uploaded-geometry and edited-scene kernels 0.5-2.4 % of kernel time or
-  // ~1.5 % of pipelined value (profiles/r05_young_cut_ab.json)
-  if (!small_launch && bpc == 8 && (kv == KV_CONST_NEE || kv == KV_CONST_NEE_REF) && SPT_YOUNG_CUT > 0) {
+  // the literal HEAD NEE kernels (and the boxes-only-uploaded one: edited scene -4 %) at 8 blocks
+  // per CU only (the measured shape): the sphere kernel (C5) lost 3.6 %, the uploaded-geometry
+  // kernels 0.5-2.4 % of kernel time or ~1.5 % of pipelined value (profiles/r05_young_cut_ab.json)
+  if (!small_launch && bpc == 8 && (kv == KV_CONST_NEE || kv == KV_CONST_NEE_REF || kv == KV_UPBOX_NEE) &&
+      SPT_YOUNG_CUT > 0) {
     K.young_block = (uint32_t)(SPT_YOUNG_RANK * c->n_cu);
     K.young_cut = (uint32_t)(n_units * (uint64_t)SPT_YOUNG_CUT / 1000u);
   }
@@ -2386,7 +2406,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
   c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
-                       kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE || kv == KV_RECTDIFF_NEE;
+                       kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE || kv == KV_RECTDIFF_NEE ||
+                       kv == KV_UPBOX_NEE;
   const int grid = c->n_cu * bpc;
   *c->h_kp = K;
   SPT_HIP(hipMemcpyAsync(c->d_kp, c->h_kp, sizeof(KParams), hipMemcpyHostToDevice, stream));
