@@ -1664,7 +1664,8 @@ static spt_status fail(spt_status s, const std::string& msg) {
 using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
        KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF,
-       KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_UPBOX_NEE, KV_COUNT };
+       KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_UPBOX_NEE, KV_UPBOX_COS,
+       KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
@@ -1674,7 +1675,7 @@ static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoCornellConst, CfgHeadCosRef>, render_kernel<TopoSphDiff, CfgSphNeeRef>,
     render_kernel<TopoCornell, CfgHeadNee>, render_kernel<TopoCornell, CfgHeadCos>,
     render_kernel<TopoRectDiff, CfgHeadNee>, render_kernel<TopoRectDiff, CfgHeadCos>,
-    render_kernel<TopoCornellUpBox, CfgHeadNee>};
+    render_kernel<TopoCornellUpBox, CfgHeadNee>, render_kernel<TopoCornellUpBox, CfgHeadCos>};
 
 struct spt_context {
   int device = 0;
@@ -2225,6 +2226,13 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                  prims[p->light_id].kind == SPT_RECT_XZ
              ? (K.leak_end ? KV_SPHDIFF_NEE : KV_SPHDIFF_NEE_REF)
              : KV_SPHDIFF;
+  if (kv == KV_CORNELL_COS && kcap >= 3 && n_prims >= 7) {  // the cosine estimator: no clauses needed
+    spt_prim head[17];
+    int32_t nh = 0;
+    bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
+    for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
+    if (ok) kv = KV_UPBOX_COS;  // the room and light HEAD's: only the boxes uploaded
+  }
   // The sphere NEE kernel's early resolve needs the HEAD room (rect[] :287-294, light at index 6)
   // as prims 0..6, nothing else but narrow spheres, and a threshold above every sphere's top
   // (early_room_proven); otherwise it stays off (+inf) and every shadow ray is traced.

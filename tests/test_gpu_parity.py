@@ -571,8 +571,8 @@ def test_other_topology_rect_scene_bit_exact(spt, oracle, kernel, nee):
 @pytest.mark.parametrize("nee", [1.0, 0.0])
 def test_edited_cornell_scene_bit_exact(spt, oracle, kernel, nee):
     """rect[] edited (the short box moved 1 unit in x): the HEAD topology with uploaded geometry --
-    auto = the room and light literal with the boxes uploaded (KV_UPBOX_NEE; cosine only:
-    KV_CORNELL_COS), const = the estimator-specialised uploaded-geometry kernels (KV_CORNELL_NEE /
+    auto = the room and light literal with the boxes uploaded (KV_UPBOX_NEE / KV_UPBOX_COS), const =
+    the estimator-specialised uploaded-geometry kernels (KV_CORNELL_NEE /
     _COS), cornell = the run-time-estimator one. Image and statistics equal the oracle's."""
     prims = spt.move_short_box(spt.cornell_scene(), 1.0)
     p = spt.default_params(width=64, height=48, spp=16, seed=3, nee_prob=nee,
