@@ -603,15 +603,17 @@ def test_full_size_scheduling_never_changes_results(spt, flags):
     assert sa["samples"] == w * h * spp
 
 
+@pytest.mark.parametrize("kernel", ["auto", "const"])
 @pytest.mark.parametrize("edit", range(5))
-def test_edited_scene_early_resolve_matches_oracle_proof(spt, oracle, edit):
+def test_edited_scene_early_resolve_matches_oracle_proof(spt, oracle, edit, kernel):
     """An edited rect[] of the HEAD topology (boxes moved: every clause of early_geo_proven occurs)
-    on the uploaded-geometry NEE kernel: image and statistics bit-exact, and the shadow rays it
-    resolved without a trace are exactly the oracle's claims, none contradicted."""
+    on the boxes-only-uploaded NEE kernel (auto, KV_UPBOX_NEE) and on the uploaded-geometry one
+    (const, KV_CORNELL_NEE): image and statistics bit-exact, and the shadow rays it resolved without
+    a trace are exactly the oracle's claims, none contradicted."""
     import test_oracle as to
 
     prims = to._move_boxes(spt, **to.EDITS[edit])
-    p = spt.default_params(width=96, height=72, spp=16, seed=2 + edit)
+    p = spt.default_params(width=96, height=72, spp=16, seed=2 + edit, flags=spt.kernel_flag(kernel))
     oracle.proof_check(True, edited=True)
     try:
         gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
