@@ -286,6 +286,9 @@ spt_status spt_write_image(int32_t device, const float* rgb, int32_t w, int32_t 
 
 /* ---- introspection ---- */
 int32_t spt_abi_version(void);
+/* sha256[:16] of the kernel sources this library was built from (the Makefile's HASHED list; equals
+ * the Python package's kernel_sources_sha16() over an unchanged tree). */
+const char* spt_build_sources_sha16(void);
 const char* spt_status_string(spt_status s);
 const char* spt_last_error(void); /* thread-local text of the last failure */
 int32_t spt_device_count(void);

@@ -106,7 +106,8 @@ EXPORTS = ["spt_default_params", "spt_camera_init", "spt_scene_cornell", "spt_sc
            "spt_encoder_create", "spt_encoder_destroy", "spt_encode_image", "spt_write_image",
            "spt_comm_unique_id", "spt_comm_create", "spt_comm_destroy", "spt_comm_reserve",
            "spt_gather_framebuffer", "spt_deinterleave_rows", "spt_render_multi", "spt_shutdown",
-           "spt_gather_plan", "spt_gather_staging_floats", "spt_deinterleave_source"]
+           "spt_gather_plan", "spt_gather_staging_floats", "spt_deinterleave_source",
+           "spt_build_sources_sha16"]
 IMAGE_FORMATS = {"p3": 0, "p6": 1, "pfm": 2}
 FLAG_UNIFORM_SCATTER = 1  # spt_params.flags: random_scattering from the uniform code of :352-359
 # spt_params.flags: leaked paths go on from the miss vertex as the reference's (:371-377) instead of
@@ -160,6 +161,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                      P(spt_params), ctypes.c_void_p, ctypes.c_void_p]
     lib.spt_context_stats.argtypes = [ctypes.c_void_p, P(spt_stats)]
     lib.spt_abi_version.restype = I32
+    lib.spt_build_sources_sha16.restype = ctypes.c_char_p
     lib.spt_status_string.argtypes = [I32]
     lib.spt_status_string.restype = ctypes.c_char_p
     lib.spt_last_error.restype = ctypes.c_char_p
@@ -224,6 +226,11 @@ def kernel_sources_sha16() -> str:
         with open(os.path.join(_HERE, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
+
+
+def build_sources_sha16() -> str:
+    """kernel_sources_sha16() of the sources the loaded libspt.so was built from (embedded by make)."""
+    return load_library().spt_build_sources_sha16().decode()
 
 
 def _release_dropin_contexts() -> None:

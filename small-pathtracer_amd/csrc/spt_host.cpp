@@ -204,6 +204,10 @@ extern "C" int32_t spt_shard_rows(const spt_params* p, int32_t* rows_out, int32_
 int spt_shard_row_count(const spt_params* p) { return spt_shard_rows(p, nullptr, 0); }
 
 extern "C" int32_t spt_abi_version(void) { return SPT_ABI_VERSION; }
+#ifndef SPT_SOURCES_SHA16
+#define SPT_SOURCES_SHA16 "unknown"
+#endif
+extern "C" const char* spt_build_sources_sha16(void) { return SPT_SOURCES_SHA16; }
 
 extern "C" const char* spt_status_string(spt_status s) {
   switch (s) {

@@ -32,6 +32,7 @@ def test_exports_every_declared_symbol(spt):
 def test_abi_version_and_status_strings(spt):
     lib = spt.load_library()
     assert lib.spt_abi_version() == 5
+    assert len(lib.spt_build_sources_sha16()) == 16
     for code, text in spt.STATUS.items():
         assert lib.spt_status_string(code).decode() == text
 
