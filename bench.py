@@ -221,6 +221,7 @@ def image_writer(spt, full, w, h, with_cpu: bool):
 
     enc = spt.Encoder(torch.cuda.current_device())
     out = {}
+    p3_dev = b""  # the GPU encoder's P3 bytes of the bench image (compared with the CPU writer's)
     try:
         for name in ("p3", "p6", "pfm"):
             cap = spt.Encoder.bound(w, h, name)
@@ -234,6 +235,8 @@ def image_writer(spt, full, w, h, with_cpu: bool):
                 n = enc.encode(full.data_ptr(), w, h, name, buf.data_ptr(), cap, stream)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / reps
+            if name == "p3" and with_cpu:
+                p3_dev = buf[:n].cpu().numpy().tobytes()
             moved = w * h * 12 * (2 if name == "p3" else 1) + n
             out[name] = {"bytes": n, "ms": round(dt * 1e3, 4), "GBps": round(moved / dt / 1e9, 1)}
         # the C4/C5 image size (4096^2, 201 MB of fp32) with synthetic data, P3
@@ -257,7 +260,8 @@ def image_writer(spt, full, w, h, with_cpu: bool):
             b = oracle.encode_image(img, 0)
             out["p3"]["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
             out["p3"]["cpu_kind"] = "oracle snprintf restatement of :548-551, 1 thread"
-            out["p3"]["bytes_equal_cpu"] = bool(len(b) == out["p3"]["bytes"])
+            # byte for byte: the device buffer the GPU encoder wrote against the CPU writer's bytes
+            out["p3"]["bytes_equal_cpu"] = bool(b == p3_dev)
     finally:
         enc.close()
     return out
@@ -540,14 +544,15 @@ def main() -> None:
     kstats = []
     n_step = [0]
 
-    def step():
+    def step(p_=None):
         k = n_step[0]
         n_step[0] += 1
         i = k % nfly
         s_ = streams[i]
         if gather_done[i] is not None:  # buffer i's previous gather must have read it
             s_.wait_event(gather_done[i])
-        rens[k % n_ctx].render_async(prims, cam, params, shards[i].data_ptr(), s_.cuda_stream)
+        rens[k % n_ctx].render_async(prims, cam, params if p_ is None else p_, shards[i].data_ptr(),
+                                     s_.cuda_stream)
         if k >= lag:  # the statistics of the step `lag` back (its context's last launch)
             kstats.append(rens[(k - lag) % n_ctx].stats())
         if comm is not None or use_torch_gather:
@@ -734,27 +739,6 @@ def main() -> None:
             one = spt.render(prims, cam, p1)
             gather_exact = bool(np.array_equal(one, img))
             assert gather_exact, "gathered image differs from the 1-GPU render"
-        # Contract v6's leak-end rule, quantified on this workload: the same render
-        # with leaked paths going on as the reference's (SPT_FLAG_REFERENCE_LEAKS; the same Philox
-        # streams, so only the leaked paths differ), after the timed region
-        leak = None
-        if world == 1 and cfg["scene"] == "cornell":
-            if args.reference_leaks:
-                leak = {"rule": "off: leaked paths go on from the miss vertex as the reference's "
-                                "(:371-377, SPT_FLAG_REFERENCE_LEAKS)"}
-            else:
-                pr = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
-                                        max_depth=cfg["max_depth"], tile_rows=8, device=local,
-                                        flags=spt.FLAG_REFERENCE_LEAKS)
-                img_r, st_r = spt.render(prims, cam, pr, return_stats=True)
-                leak = {"rule": "contract v6: a leaked path ends at its first miss (DESIGN.md §3); "
-                                "the reference wanders on from the miss vertex (:371-377)",
-                        "reference_vertices_per_sample": round(st_r["vertices"] / my_samples, 4),
-                        "reference_vertices_skipped_frac": round(1 - s0["vertices"] / st_r["vertices"], 4),
-                        "reference_path_rays_skipped_frac": round(1 - s0["path_rays"] / st_r["path_rays"], 4),
-                        "image_mean_rel_diff": float(f"{(img.mean() - img_r.mean()) / img_r.mean():.3g}"),
-                        "how": "one render of this workload with SPT_FLAG_REFERENCE_LEAKS (same seed, "
-                               "same random streams) after the timed region"}
         cpu = None
         port = None
         if not args.no_cpu_baseline and world == 1:
@@ -782,6 +766,56 @@ def main() -> None:
         if qual is not None and port is not None:
             # the bench's own rows re-rendered by the CPU contract (cpu_baseline.port): exact
             qual["rmse_vs_contract"] = 0.0 if port.get("gpu_pixels_bit_exact") else None
+        # Contract v6's leak-end rule, quantified on this workload: the same workload
+        # with leaked paths going on as the reference's (SPT_FLAG_REFERENCE_LEAKS; the same Philox
+        # streams, so only the leaked paths differ), timed after everything above has read the
+        # bench image: K steps through the same pipeline (value_reference_leaks) and 3 isolated
+        # launches (kernel_ms_reference_leaks), VERDICT r05 item 4
+        leak = None
+        if world == 1 and cfg["scene"] == "cornell":
+            if args.reference_leaks:
+                leak = {"rule": "off: leaked paths go on from the miss vertex as the reference's "
+                                "(:371-377, SPT_FLAG_REFERENCE_LEAKS)"}
+            else:
+                pr = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
+                                        max_depth=cfg["max_depth"], tile_rows=8, device=local,
+                                        chunk=args.chunk,
+                                        flags=spt.kernel_flag(args.kernel_level) | spt.FLAG_REFERENCE_LEAKS)
+                saved = list(kstats)
+                kstats.clear()
+                for _ in range(n_warm):
+                    step(pr)
+                drain()
+                kstats.clear()
+                torch.cuda.synchronize()
+                t_r = time.perf_counter()
+                for _ in range(args.steps):
+                    step(pr)
+                torch.cuda.synchronize()
+                el_r = time.perf_counter() - t_r
+                drain()
+                st_r = kstats[-1]
+                img_r = fulls[(args.steps - 1) % nfly].cpu().numpy()
+                iso_r = []
+                for _ in range(3):
+                    rens[0].render_async(prims, cam, pr, shards[0].data_ptr(), streams[0].cuda_stream)
+                    iso_r.append(rens[0].stats()["kernel_ms"])
+                torch.cuda.synchronize()
+                kstats[:] = saved
+                leak = {"rule": "contract v6: a leaked path ends at its first miss (DESIGN.md §3); "
+                                "the reference wanders on from the miss vertex (:371-377)",
+                        "value_reference_leaks": round(samples_per_step * args.steps / el_r / 1e6, 3),
+                        "ms_per_step_reference_leaks": round(el_r / args.steps * 1e3, 3),
+                        "kernel_ms_reference_leaks": round(float(np.mean(iso_r)), 3),
+                        "kernel_ratio_reference_leaks": round(float(np.mean(iso_r)) / float(kms.mean()), 4),
+                        "reference_vertices_per_sample": round(st_r["vertices"] / my_samples, 4),
+                        "reference_vertices_skipped_frac": round(1 - s0["vertices"] / st_r["vertices"], 4),
+                        "reference_path_rays_skipped_frac": round(1 - s0["path_rays"] / st_r["path_rays"], 4),
+                        "image_mean_rel_diff": float(f"{(img.mean() - img_r.mean()) / img_r.mean():.3g}"),
+                        "how": f"the same workload with SPT_FLAG_REFERENCE_LEAKS (same seed, same random "
+                               f"streams) after the timed region: {args.steps} steps through the same "
+                               f"pipeline ({nfly} frames in flight) after {n_warm} warm-up steps, and 3 "
+                               f"launches one at a time for the kernel time"}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": n_warm,
