@@ -368,6 +368,17 @@ def main() -> None:
     ap.add_argument("--move-box", type=float, default=0.0,
                     help="edit rect[] (:287-311): move the short box by this many units in x (the "
                          "HEAD topology with uploaded geometry; 0 = the reference's table)")
+    ap.add_argument("--light-y", type=float, default=None,
+                    help="edit rect[] (:294): the light's plane y (81.5 in the reference; the light "
+                         "uploaded, the room literal: KV_UPBOX_*)")
+    ap.add_argument("--light-grow", type=float, default=0.0,
+                    help="edit rect[] (:294): grow the light rectangle by this much on every side")
+    ap.add_argument("--room-depth", type=float, default=None,
+                    help="edit rect[] (:288-293): the back wall's z (170 in the reference; the room "
+                         "uploaded too: KV_CORNELL_*)")
+    ap.add_argument("--camera", choices=["reference", "tilted"], default="reference",
+                    help="tilted: Camera(lookfrom (50,40,168), lookat (56,36,5), vup (0,1,0)), not "
+                         "axis-aligned (the literal kernels' any-camera forms, Cfg CAMAX 2)")
     ap.add_argument("--drop-short-box", action="store_true",
                     help="edit rect[] (:287-311): remove the short box (:305-309), another topology "
                          "(the uploaded-geometry rect-only kernels)")
@@ -458,9 +469,20 @@ def main() -> None:
     if args.drop_short_box:
         assert cfg["scene"] == "cornell", "--drop-short-box edits the Cornell scene"
         prims = spt.drop_short_box(prims)
-    edited = bool(args.move_box or args.drop_short_box)
+    if args.room_depth is not None:
+        assert cfg["scene"] == "cornell", "--room-depth edits the Cornell scene"
+        prims = spt.edit_room(prims, depth=args.room_depth)
+    if args.light_y is not None or args.light_grow:
+        assert cfg["scene"] == "cornell", "--light-y / --light-grow edit the Cornell scene"
+        gl = args.light_grow
+        prims = spt.edit_light(prims, x=(32 - gl, 68 + gl), z=(63 - gl, 96 + gl),
+                               y=81.5 if args.light_y is None else args.light_y)
+    edited = bool(args.move_box or args.drop_short_box or args.room_depth is not None
+                  or args.light_y is not None or args.light_grow)
     w, h = cfg["width"], cfg["height"]
-    cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    cam_kw = dict(lookat=(56, 36, 5)) if args.camera == "tilted" else {}
+    cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)), **cam_kw)
+    edited = edited or args.camera != "reference"
     leak_flag = spt.FLAG_REFERENCE_LEAKS if args.reference_leaks else 0
     params = spt.default_params(width=w, height=h, spp=spp, nee_prob=cfg["nee_prob"],
                                 max_depth=cfg["max_depth"], tile_rows=8, shard_index=rank,
@@ -830,6 +852,12 @@ def main() -> None:
                                                    if scaling == "weak" and world > 1 else "")
                        + (f", short box moved {args.move_box:g} in x (edited rect[])" if args.move_box else "")
                        + (", short box removed (edited rect[])" if args.drop_short_box else "")
+                       + (f", back wall at z = {args.room_depth:g} (edited rect[])"
+                          if args.room_depth is not None else "")
+                       + (f", light at y = {81.5 if args.light_y is None else args.light_y:g} grown by "
+                          f"{args.light_grow:g} (edited rect[])"
+                          if args.light_y is not None or args.light_grow else "")
+                       + (", tilted camera (lookat (56,36,5))" if args.camera == "tilted" else "")
                        + (", leaked paths as the reference's" if args.reference_leaks else ""),
                        "width": w, "height": h, "spp": spp,
                        "estimator": "nee" if cfg["nee_prob"] >= 1 else "cosine",

@@ -657,6 +657,10 @@ typedef struct {
      choice in spt_render_async, the kernel's early_geo_proven) */
   float eb_top[2], eb_sgn[2], eb_bnd[2];
   int eb_z[2];
+  /* ... and its room clause (round 6: the room and the light may be edited too): the vertex lies in
+     [lo, hi] per axis as (bits(v) - er_lo) <= er_span on the float bits (lo >= +0), y below the
+     light plane */
+  uint32_t er_lo[3], er_span[3];
   int unit;     /* c_unit_dirs: 1 = unit directions, 0 = the free-scale contract */
   float nee_c;  /* free-scale NEE weight constant: light_area / pi, rounded once */
 } c_ctx;
@@ -1042,29 +1046,72 @@ static int g_proof_on; /* 1: the HEAD scene (boxes); 2: spheres below g_proof_y0
                           3: an edited HEAD-topology rect[] (c_find_early_clauses) */
 static float g_proof_y0;
 static uint64_t g_proof_n, g_proof_bad;
-/* The clauses of early_geo_proven (spt_kernel.hip) for a scene with two boxes (c_find_boxes), as the
- * host picks them from the reference's wrapped light samples (x in [31, 33), z in [62, 64)): a box
- * with x0 >= 33 is clear for x <= x0, x1 <= 31 for x >= x1, z0 >= 64 for z <= z0, z1 <= 62 for
- * z >= z1, any box for a vertex at or above its top (below the light plane 81.5); +inf / -inf: no
- * clause. Whether the scene qualifies at all (the HEAD room and light) is the caller's test. */
+/* The clauses of early_geo_proven (spt_kernel.hip) for a scene with a room (c_find_room), two boxes
+ * (c_find_boxes) and an XZ light, as the host picks them (spt_render_async, early_geo_setup):
+ *  - room: the vertex in the room's box, y below the light plane: X0 <= x <= X1, Y0 <= y < y_L,
+ *    Z0 <= z <= Z1 (uint compares of the float bits, so X0, Y0, Z0 >= 0). From inside, the room's
+ *    slab candidate is its exit face; with the light's rectangle >= 1 inside the side walls, the
+ *    ceiling >= 0.05 above the light plane and the room < 1000 across, every exit face lies beyond
+ *    the light crossing by a relative margin >= 5e-5, far above the keys' 2^-17 resolution (HEAD:
+ *    31 / 63 units and 0.1 above; the literal kernel's early_nee_proven is this clause for HEAD);
+ *  - the light plane y_L at most 81.5 = the reference's sample plane y = 81.6 (:367) less 0.1, so
+ *    the crossing lies on the segment from the vertex to its light sample (x in [31, 33), z in
+ *    [62, 64): the reference's wrapped samples), and at least 1 above the floor;
+ *  - per box, a top >= 0.5 below the light plane, and the clause its position allows: x0 >= 33 ->
+ *    clear for x <= x0 (the segment to the sample stays at x <= x0), x1 <= 31 for x >= x1, z0 >= 64
+ *    for z <= z0, z1 <= 62 for z >= z1; always: a vertex at or above its top (the ray rises).
+ * A scene that fails any condition gets no clause: +inf / -inf (nothing is resolved early). */
 static void c_find_early_clauses(c_ctx* C) {
-  int b, ok = C->n_box == 2;
+  int b, a, ok = C->n_box == 2 && C->room[0] >= 0;
+  const int l = C->P->light_id;
+  float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, yl = 0;
   for (b = 0; b < 2; b++) {
     C->eb_top[b] = INFINITY; C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = -INFINITY; C->eb_z[b] = 0;
+  }
+  for (a = 0; a < 3; a++) C->er_lo[a] = C->er_span[a] = 0;
+  if (ok && (l < 0 || l >= C->n || C->prims[l].kind != SPT_RECT_XZ)) ok = 0;
+  if (ok) {
+    const c_prim* L = &C->prims[l];
+    for (a = 0; a < 3; a++) { /* room tests: XY pair (planes z), XZ (y), YZ (x) */
+      const c_test* R = &C->tests[C->room[a]];
+      const int ax = a == 0 ? 2 : (a == 1 ? 1 : 0);
+      lo[ax] = R->k0 < R->k1 ? R->k0 : R->k1;
+      hi[ax] = R->k0 < R->k1 ? R->k1 : R->k0;
+      ok = ok && lo[ax] >= 0.0f && hi[ax] - lo[ax] <= 1000.0f;
+    }
+    yl = L->k;
+    ok = ok && L->ha >= 0.0f && L->hb >= 0.0f && L->ma - L->ha >= lo[0] + 1.0f &&
+         L->ma + L->ha <= hi[0] - 1.0f && L->mb - L->hb >= lo[2] + 1.0f &&
+         L->mb + L->hb <= hi[2] - 1.0f && yl >= lo[1] + 1.0f && yl <= 81.5f && hi[1] >= yl + 0.05f;
   }
   for (b = 0; ok && b < 2; b++) {
     const c_test *XY = &C->tests[C->box[b][0]], *YZ = &C->tests[C->box[b][1]], *T = &C->tests[C->box[b][2]];
     const float z0 = XY->k0 < XY->k1 ? XY->k0 : XY->k1, z1 = XY->k0 < XY->k1 ? XY->k1 : XY->k0;
     const float x0 = YZ->k0 < YZ->k1 ? YZ->k0 : YZ->k1, x1 = YZ->k0 < YZ->k1 ? YZ->k1 : YZ->k0;
-    if (!(T->k0 < 81.5f)) { ok = 0; break; }
+    if (!(T->k0 <= yl - 0.5f)) { ok = 0; break; } /* top >= 0.5 below the light plane */
     C->eb_top[b] = T->k0;
     if (x0 >= 33.0f) { C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = x0; C->eb_z[b] = 0; }
     else if (x1 <= 31.0f) { C->eb_sgn[b] = -1.0f; C->eb_bnd[b] = -x1; C->eb_z[b] = 0; }
     else if (z0 >= 64.0f) { C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = z0; C->eb_z[b] = 1; }
     else if (z1 <= 62.0f) { C->eb_sgn[b] = -1.0f; C->eb_bnd[b] = -z1; C->eb_z[b] = 1; }
   }
-  if (!ok)
+  if (!ok) {
     for (b = 0; b < 2; b++) { C->eb_top[b] = INFINITY; C->eb_sgn[b] = 1.0f; C->eb_bnd[b] = -INFINITY; }
+    return;
+  }
+  for (a = 0; a < 3; a++) {
+    const float top = a == 1 ? nextafterf(yl, 0.0f) : hi[a]; /* y < y_L */
+    C->er_lo[a] = asu(lo[a]);
+    C->er_span[a] = asu(top) - asu(lo[a]);
+  }
+}
+/* The light's own test on (o, d) as in c_intersect (c_light_accepts), with its t (an XZ light). */
+static int c_light_test_xz(const c_ctx* C, fv o, fv d, float* tt_out) {
+  const c_prim* L = &C->prims[C->P->light_id];
+  const float tt = c_pt(L->k, o.y, spt_oracle_rcp_nr(d.y));
+  const float a = fmaf(d.x, tt, o.x - L->ma), b = fmaf(d.z, tt, o.z - L->mb);
+  *tt_out = tt;
+  return fabsf(a) <= L->ha && fabsf(b) <= L->hb && c_key(tt, C->light_pos) < C_KEY_NONE;
 }
 static int c_early_nee_proven(const c_ctx* C, fv o, fv d, float* tl) {
   const float tt = c_pt(81.5f, o.y, spt_oracle_rcp_nr(d.y));
@@ -1079,7 +1126,9 @@ static int c_early_nee_proven(const c_ctx* C, fv o, fv d, float* tl) {
   *tl = tt;
   if (g_proof_on == 2) return acc && room && o.y > g_proof_y0; /* spt_kernel.hip early_room_proven */
   if (g_proof_on == 3) { /* spt_kernel.hip early_geo_proven (an edited HEAD-topology rect[]) */
-    int b, ok = acc && room;
+    int b, a, ok = c_light_test_xz(C, o, d, tl);
+    const float v3[3] = {o.x, o.y, o.z};
+    for (a = 0; a < 3; a++) ok = ok && asu(v3[a]) - C->er_lo[a] <= C->er_span[a];
     for (b = 0; b < 2; b++) {
       const float v = C->eb_z[b] ? o.z : o.x;
       ok = ok && (o.y >= C->eb_top[b] || v * C->eb_sgn[b] <= C->eb_bnd[b]);

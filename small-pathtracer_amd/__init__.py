@@ -384,6 +384,40 @@ def move_short_box(prims: list, dx: float) -> list:
     return out
 
 
+def edit_light(prims: list, x=(32.0, 68.0), z=(63.0, 96.0), y=81.5, e=None) -> list:
+    """rect[] of :287-311 with the light (:294, prim 6) moved or resized: Rectangle_xz(x0, x1, z0,
+    z1, y) and optionally its emission e. The room and the boxes stay (the boxes-only-uploaded
+    kernels take the light from LDS; the early shadow-ray resolve needs the light's plane at most
+    81.5 and its rectangle >= 1 inside the walls)."""
+    out = [spt_prim.from_buffer_copy(p) for p in prims]
+    g = out[6].geom
+    g[0], g[1], g[2], g[3], g[4] = float(x[0]), float(x[1]), float(z[0]), float(z[1]), float(y)
+    if e is not None:
+        for i, v in enumerate(_v3(e)):
+            out[6].e[i] = v
+    return out
+
+
+def edit_room(prims: list, depth: float = 170.0, width=(1.0, 99.0), height: float = 81.6) -> list:
+    """rect[] of :287-311 with the room (:288-293, prims 0-5) resized: back wall at z = depth, side
+    walls at x = width, ceiling at y = height, every wall's extents to match (a closed room, the
+    HEAD topology)."""
+    out = [spt_prim.from_buffer_copy(p) for p in prims]
+    x0, x1 = float(width[0]), float(width[1])
+    for i in (0, 1):  # Front / Back: Rectangle_xy(x0, x1, 0, height, z)
+        g = out[i].geom
+        g[0], g[1], g[3] = x0, x1, float(height)
+    out[1].geom[4] = float(depth)
+    for i, xw in ((2, x0), (3, x1)):  # Left / Right: Rectangle_yz(0, height, 0, depth, x)
+        g = out[i].geom
+        g[1], g[3], g[4] = float(height), float(depth), xw
+    for i in (4, 5):  # Bottom / Top: Rectangle_xz(x0, x1, 0, depth, y)
+        g = out[i].geom
+        g[0], g[1], g[3] = x0, x1, float(depth)
+    out[5].geom[4] = float(height)
+    return out
+
+
 def drop_short_box(prims: list) -> list:
     """rect[] of :287-311 without the short box (:305-309, prims 12-16): another topology (the
     uploaded-geometry rect-only kernels)."""

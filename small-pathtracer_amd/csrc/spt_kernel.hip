@@ -81,7 +81,10 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 // mille of the units are handed out. The SIMD issues oldest-first, so these waves get the fewest
 // slots (C3: the two youngest of a CU's 8 blocks do ~4 % of the work) and the units they hold end
 // the launch. Round 5 A/B (profiles/r05_young_cut_ab.json): C3 isolated kernel -1.3 to -1.6 %,
-// C4 -0.8 %, values flat; applied to the literal HEAD NEE kernels only (the others lost).
+// C4 -0.8 %, values flat; applied to the literal HEAD NEE kernels and the boxes-only-uploaded NEE
+// kernel (KV_UPBOX_NEE, edited scenes: -4 %) only (the others lost). It assumes the dispatcher hands
+// each CU its blocks in blockIdx order, so blockIdx >= SPT_YOUNG_RANK x n_cu are the blocks a CU
+// received last; that holds only with every CU full at 8 blocks, so the host applies it at bpc == 8.
 #ifndef SPT_YOUNG_CUT
 #define SPT_YOUNG_CUT 300
 #endif
@@ -217,6 +220,10 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // host could not prove one, or the predicate is off)
   float eb_top[2], eb_sgn[2], eb_bnd[2];
   uint32_t eb_z[2];
+  // ... and its room clause (early_geo_setup): the vertex in the room's box below the light plane,
+  // per axis (bits(v) - er_lo) <= er_span on the float bits (HEAD: x in [1, 99], y in [0, 81.5),
+  // z in [0, 170], the literal early_room_ok); er_lo = 0, er_span = 0 with no clause
+  uint32_t er_lo[3], er_span[3];
   int unit_dirs;  // oracle c_unit_dirs: the scene has a sphere or a REFR primitive
   float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
   unsigned long long* accum;  // [n_local_pix][3] 1.31 fixed point (stolen ranges; every unit without slots)
@@ -293,7 +300,10 @@ using TopoGenericWide = Topo<-1, -1, -1, true, -1, false, -1, -1, -1, true, true
 //   NOS1:  1 = no vertex-1 stream-1 draws (rr_depth >= 1 and nee_prob is 0 or 1)
 //   CAMAX: 1 = axis-aligned camera (horizontal = (h,0,0), vertical = (0,v,0) up to the sign of
 //          zero, origin components nonzero, as the reference's :521 camera): the zero products of
-//          the camera's fma chain vanish exactly, so the ray is the same bits with 5 fewer VALU
+//          the camera's fma chain vanish exactly, so the ray is the same bits with 5 fewer VALU;
+//          2 = any camera (Camera :262-275 with any lookat/vup, round 6), its per-pixel P_x, P_y,
+//          P_z per work unit and the jitter's Cu, Cv in SGPRs: 6 fmas per camera ray (1: 2,
+//          0/-1: 12 and scalar loads); the same bits as the general form (contract v5)
 //   LREF:  1 = the reference's light sampling and RR constants (light x0/dx 32/36, z0/dz 63/36,
 //          y 81.6, area 1296 :365-367,:471; light id 6 :467; rr_depth 5 :448): literals instead
 //          of scalar loads in the loop
@@ -311,6 +321,9 @@ using CfgRuntime = Cfg<-1, -1, -1, -1, -1, -1>;
 using CfgHeadNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 1>;
 using CfgHeadCos = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 1>;
 using CfgHeadNeeRef = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 0>;
+// the same estimators with any camera (a tilted lookat)
+using CfgHeadNeeCam = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 2, 1, 1>;
+using CfgHeadCosCam = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 2, 1, 1>;
 using CfgHeadCosRef = Cfg<0, SPT_LIGHT_GLIBC_WRAP, 1, 1, 1, 1, 1, 0>;
 // Sphere scenes with the reference's NEE estimator and black light (C5): early NEE resolve
 using CfgSphNee = Cfg<1, SPT_LIGHT_GLIBC_WRAP, 1, -1, -1, -1, 1, 1>;
@@ -527,6 +540,23 @@ __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   const bool ia = fabsf(a) <= g->ha, ib = fabsf(b) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib), a};
 }
+// The uploaded light of the boxes-only-uploaded kernels (a single XZ test at the HEAD light's grouped
+// position, from LDS): rect_cand's arithmetic for a single, with the position literal.
+template <class GT>
+__device__ __forceinline__ void light_cand(const GT& g, const Ray6& r, uint32_t& tmin) {
+  const float t0 = plane_t(g.k0 - r.oa, r.ia);
+  const float a = fmaf(r.db, t0, r.ob - g.ma), b = fmaf(r.dc, t0, r.oc - g.mb);
+  const bool inb = (bool)((int)(fabsf(a) <= g.ha) & (int)(fabsf(b) <= g.hb));
+  tmin = umin(tmin, inb ? key_c<kCornellLightPos>(t0) : 0xFFFFFFFFu);
+}
+// The same light's own test (rect_eval on a GeoTest): t and whether the in-plane test accepts.
+template <class GT>
+__device__ __forceinline__ RectHit rect_eval_test(const GT& g, const Ray6& r) {
+  const float tt = plane_t(g.k0 - r.oa, r.ia);
+  const float a = fmaf(r.db, tt, r.ob - g.ma), b = fmaf(r.dc, tt, r.oc - g.mb);
+  const bool ia = fabsf(a) <= g.ha, ib = fabsf(b) <= g.hb;
+  return RectHit{tt, (bool)((int)ia & (int)ib), a};
+}
 // A candidate at t with position pos can be the nearest hit at all: its key
 // (bits(t) | 63) ^ (63 - pos) ranks below kKeyNone = bits(1e20) | 63, i.e. bits(t) <= kKeyNone for
 // pos < 63 (one compare) and bits(t) < kKeyNone & ~63 for pos 63.
@@ -613,13 +643,15 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     const Ray6 rays[3] = {ray6<0>(o, d, ix, iy, iz), ray6<1>(o, d, ix, iy, iz),
                           ray6<2>(o, d, ix, iy, iz)};
     cornell_room(rays, tmin);
-    cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);
     if constexpr (TP::UPBOX) {
       // the uploaded HEAD-topology tests (host-checked: n_txy 0, n_txz 1, n_tyz 0): the light, the
-      // room's three pairs (its XZ pair's k0 the floor), then the two boxes' three tests each
+      // room's three pairs (its XZ pair's k0 the floor), then the two boxes' three tests each. The
+      // room is literal (HEAD's, host-checked); the light and the boxes come from LDS.
+      light_cand(tests[0], rays[1], tmin);
       geo_box(tests + 4, tests + 2, rays[2], rays[1], rays[0], tmin);
       geo_box(tests + 7, tests + 2, rays[2], rays[1], rays[0], tmin);
     } else {
+      cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);  // the light
       cornell_boxes(std::make_integer_sequence<int, kCornellBoxes.n>{}, rays, tmin);
     }
   } else {
@@ -767,15 +799,25 @@ __device__ __forceinline__ bool early_room_proven(f3 x, float y0) {
 // (Round 4: the short box's "x_L < 63" is implied below y = 25: the reference's wrapped light
 // samples lie at x in [31, 33), and the crossing of y = 81.5 lies within 0.1 / (81.6 - y) < 0.0018
 // of the way back to the vertex, so x_L < 33.2 there. One compare fewer; the same predicate.)
-// The same proof for an edited rect[] of the HEAD topology (the uploaded-geometry kernels): the
-// HEAD room and light unchanged (host-checked), each box standing on the floor below the light
+// The same proof for an edited rect[] of the HEAD topology (the uploaded-geometry kernels; round 6:
+// the room and the light may be edited as well): the vertex in the room's box below the light plane
+// (early_room_ok_k: the room's exit face lies beyond the light crossing, the host checks the light's
+// margins to the walls and the ceiling), each box standing on the floor >= 0.5 below the light
 // plane with a clause the host picks from the reference's wrapped light samples (x in [31, 33),
-// z in [62, 64)): a box with x0 >= 33 is clear for a vertex with x <= x0 (the segment to the light
-// stays at x <= x0) -- the HEAD short box's clause --, x1 <= 31 for x >= x1, z0 >= 64 for z <= z0,
-// z1 <= 62 for z >= z1 (the HEAD tall box's); and every box for a vertex at or above its top.
+// z in [62, 64), y 81.6; the light plane at most 81.5, so the crossing lies on the segment to the
+// sample): a box with x0 >= 33 is clear for a vertex with x <= x0 (the segment to the light stays at
+// x <= x0) -- the HEAD short box's clause --, x1 <= 31 for x >= x1, z0 >= 64 for z <= z0, z1 <= 62
+// for z >= z1 (the HEAD tall box's); and every box for a vertex at or above its top.
 // The oracle restates the choice (c_find_early_clauses) and checks every claim (test_oracle.py).
+// The room clause of an edited scene (room and light from KParams, host early_geo_setup): the same
+// compares as early_room_ok with the bounds in SGPRs.
+__device__ __forceinline__ int early_room_ok_k(f3 x, const SPT_CONST KParams* P) {
+  return (int)(__float_as_uint(x.x) - P->er_lo[0] <= P->er_span[0]) &
+         (int)(__float_as_uint(x.y) - P->er_lo[1] <= P->er_span[1]) &
+         (int)(__float_as_uint(x.z) - P->er_lo[2] <= P->er_span[2]);
+}
 __device__ __forceinline__ bool early_geo_proven(f3 x, const SPT_CONST KParams* P) {
-  int ok = early_room_ok(x);
+  int ok = early_room_ok_k(x, P);
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const float v = P->eb_z[b] ? x.z : x.x;
@@ -949,6 +991,7 @@ render_kernel(const KParams* __restrict__ Pg) {
   // camera raster terms of the unit's pixel, fx = (x - 0.5) - 128, fy = (h - y - 1 - 0.5) - 128;
   // the axis-aligned camera kernels hold P_x, P_y (jitter_f) here instead
   float fx = 0.0f, fy = 0.0f;
+  float fz = 0.0f;  // CAMAX 2: P_z (fx, fy hold P_x, P_y)
   unsigned long long acc0 = 0, acc1 = 0, acc2 = 0;
   // o starts at the camera (the first ray of every sample is a camera ray; the path end resets it)
   f3 o = mk(cptr(Pg)->cam[0], cptr(Pg)->cam[1], cptr(Pg)->cam[2]);
@@ -964,6 +1007,15 @@ render_kernel(const KParams* __restrict__ Pg) {
     const SPT_CONST KParams* C = cptr(Pg);
     ck = CamK{C->cam[0], C->cam[1], C->cam[2], C->cam_au[0], C->cam_av[1], C->cam_cu[0],
               C->cam_cv[1], C->cam_l[0], C->cam_l[1], C->cam_l[2], C->fix_scale};
+  }
+  // CAMAX 2 (any camera): origin, Cu, Cv and the fixed-point scale in SGPRs (Au, Av, L are read at
+  // the refill only)
+  struct CamG { float o0, o1, o2, cu0, cu1, cu2, cv0, cv1, cv2, fs; };
+  CamG cg{};
+  if constexpr (CF::CAMAX == 2) {
+    const SPT_CONST KParams* C = cptr(Pg);
+    cg = CamG{C->cam[0], C->cam[1], C->cam[2], C->cam_cu[0], C->cam_cu[1], C->cam_cu[2],
+              C->cam_cv[0], C->cam_cv[1], C->cam_cv[2], C->fix_scale};
   }
   uint32_t pool_next = 0, pool_end = 0, grab_at = 0;  // grab_at: the wave's last queue position
   bool exhausted = false, capped = false;
@@ -1065,6 +1117,11 @@ render_kernel(const KParams* __restrict__ Pg) {
         if constexpr (CF::CAMAX == 1) {  // the per-pixel P_x, P_y of the camera ray (jitter_f)
           fx = fmaf(ck.aux, fx, ck.lx);
           fy = fmaf(ck.avy, fy, ck.ly);
+        } else if constexpr (CF::CAMAX == 2) {  // P_c = fma(Au_c, fx, fma(Av_c, fy, L_c)), c = x, y, z
+          const float rx = fx, ry = fy;
+          fx = fmaf(Q->cam_au[0], rx, fmaf(Q->cam_av[0], ry, Q->cam_l[0]));
+          fy = fmaf(Q->cam_au[1], rx, fmaf(Q->cam_av[1], ry, Q->cam_l[1]));
+          fz = fmaf(Q->cam_au[2], rx, fmaf(Q->cam_av[2], ry, Q->cam_l[2]));
         }
         lp = u | 0x80000000u;  // the owner keeps its unit index: the sums go to the unit's slot
         ls = kStCam;
@@ -1101,6 +1158,8 @@ render_kernel(const KParams* __restrict__ Pg) {
           const uint32_t d_lo = (uint32_t)__builtin_amdgcn_readlane((int)pk.lo, dl);
           const float d_fx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fx), dl));
           const float d_fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy), dl));
+          float d_fz = 0.0f;
+          if constexpr (CF::CAMAX == 2) d_fz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fz), dl));
           const bool tk = lane == (uint32_t)il;  // the taker
           s_end = tk ? dend : (lane == (uint32_t)dl ? mid : s_end);
           s = tk ? mid : s;
@@ -1110,6 +1169,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           pk.lo = tk ? d_lo : pk.lo;
           fx = tk ? d_fx : fx;
           fy = tk ? d_fy : fy;
+          if constexpr (CF::CAMAX == 2) fz = tk ? d_fz : fz;
           ls = tk ? kStCam : ls;
         }
       }
@@ -1140,6 +1200,9 @@ render_kernel(const KParams* __restrict__ Pg) {
           // the zero terms vanish exactly: fma(F, +-0, y) == y and fma(+-0, f, L) == L for the
           // nonzero y, L the host checks (cam_axis)
           vc = mk(fmaf(Fu, ck.cux, fx), fmaf(Fv, ck.cvy, fy), ck.lz);
+        } else if constexpr (CF::CAMAX == 2) {  // the general form with P_c per unit
+          vc = mk(fmaf(Fv, cg.cv0, fmaf(Fu, cg.cu0, fx)), fmaf(Fv, cg.cv1, fmaf(Fu, cg.cu1, fy)),
+                  fmaf(Fv, cg.cv2, fmaf(Fu, cg.cu2, fz)));
         } else {
           float vv[3];
 #pragma unroll
@@ -1407,8 +1470,10 @@ render_kernel(const KParams* __restrict__ Pg) {
             // a miss keeps id (:466-467), so a vertex ON the light always traces its shadow ray
             bool la, early = false;
             if constexpr (kEarlyNee) {  // the light's own test (light_accepts), keeping t and a
-              const RectHit h = rect_eval(CornellRectPtr{kCornellLightPos},
-                                          Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
+              const Ray6 rl6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z};
+              RectHit h;
+              if constexpr (TP::UPBOX) h = rect_eval_test(s_test[0], rl6);  // the uploaded light
+              else h = rect_eval(CornellRectPtr{kCornellLightPos}, rl6);
               la = h.inb & key_valid(h.tt, kCornellLightPos);
               if constexpr (TP::UPBOX) early = la & early_geo_proven(x, D);
               else early = la & early_nee_proven(x);
@@ -1493,7 +1558,7 @@ render_kernel(const KParams* __restrict__ Pg) {
           ls = kStSpec;
         } else {
           SPT_REGION(9);
-          const float scale = CF::CAMAX == 1 ? ck.fs : cptr(Pg)->fix_scale;
+          const float scale = CF::CAMAX == 1 ? ck.fs : (CF::CAMAX == 2 ? cg.fs : cptr(Pg)->fix_scale);
           acc0 += fix31(L.x, scale);
           acc1 += fix31(L.y, scale);
           acc2 += fix31(L.z, scale);
@@ -1503,7 +1568,9 @@ render_kernel(const KParams* __restrict__ Pg) {
           dp1 = 1;
           {
             const SPT_CONST KParams* C = cptr(Pg);
-            o = CF::CAMAX == 1 ? mk(ck.o0, ck.o1, ck.o2) : mk(C->cam[0], C->cam[1], C->cam[2]);
+            o = CF::CAMAX == 1   ? mk(ck.o0, ck.o1, ck.o2)
+                : CF::CAMAX == 2 ? mk(cg.o0, cg.o1, cg.o2)
+                                 : mk(C->cam[0], C->cam[1], C->cam[2]);
           }
           if (TP::MAT) branch = 0;
           ls = kStCam;
@@ -1665,7 +1732,7 @@ using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
        KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF,
        KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_UPBOX_NEE, KV_UPBOX_COS,
-       KV_COUNT };
+       KV_CONST_NEE_CAM, KV_CONST_COS_CAM, KV_UPBOX_NEE_CAM, KV_UPBOX_COS_CAM, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
@@ -1675,7 +1742,9 @@ static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoCornellConst, CfgHeadCosRef>, render_kernel<TopoSphDiff, CfgSphNeeRef>,
     render_kernel<TopoCornell, CfgHeadNee>, render_kernel<TopoCornell, CfgHeadCos>,
     render_kernel<TopoRectDiff, CfgHeadNee>, render_kernel<TopoRectDiff, CfgHeadCos>,
-    render_kernel<TopoCornellUpBox, CfgHeadNee>, render_kernel<TopoCornellUpBox, CfgHeadCos>};
+    render_kernel<TopoCornellUpBox, CfgHeadNee>, render_kernel<TopoCornellUpBox, CfgHeadCos>,
+    render_kernel<TopoCornellConst, CfgHeadNeeCam>, render_kernel<TopoCornellConst, CfgHeadCosCam>,
+    render_kernel<TopoCornellUpBox, CfgHeadNeeCam>, render_kernel<TopoCornellUpBox, CfgHeadCosCam>};
 
 struct spt_context {
   int device = 0;
@@ -2031,6 +2100,83 @@ static bool cornell_const_match(const SceneGeo& g, int light_pos) {
   return true;
 }
 
+// The room of a HEAD-topology scene is the reference's (:288-293): its three pair tests at HEAD's
+// grouped positions with HEAD's fp32 geometry (materials may differ). The boxes-only-uploaded
+// kernels (TopoCornellUpBox) take the room as literals and everything else from LDS.
+static bool cornell_room_match(const SceneGeo& g) {
+  if (g.n_xy != kCornellNXY || g.n_xz != kCornellNXZ || g.n_yz != kCornellNYZ || g.n_sph != 0 ||
+      !g.has_room || g.n_txy != 0 || g.n_txz != 1 || g.n_tyz != 0 || g.n_box != 2)
+    return false;
+  const int nt = g.n_txy + g.n_txz + g.n_tyz;
+  for (int r = 0; r < 3; ++r) {
+    const CTest& C = kCornellTests.t[kCornellRoom[r]];
+    if (g.test[nt + r].pos0 != C.pos0 || g.test[nt + r].pos1 != C.pos1) return false;
+    for (const int pos : {C.pos0, C.pos1}) {
+      const GeoRect& R = g.rect[pos];
+      const CRect& H = kCornellRects[pos];
+      const float a[5] = {R.k, R.ma, R.ha, R.mb, R.hb}, b[5] = {H.k, H.ma, H.ha, H.mb, H.hb};
+      if (std::memcmp(a, b, sizeof a) != 0 || R.idx != H.idx) return false;
+    }
+  }
+  return true;
+}
+
+// The early resolve's clauses for a HEAD-topology scene with the reference's estimator (oracle
+// c_find_early_clauses, which the proof tests check claim by claim): the room's box with y below
+// the light plane (early_room_ok_k), the light's rectangle >= 1 inside the side walls and >= 1 above
+// the floor, its plane <= 81.5 (0.1 below the reference's sample plane :367) and >= 0.05 below the
+// ceiling, the room < 1000 across with X0, Y0, Z0 >= 0; per box a top >= 0.5 below the light plane
+// and the clause its position allows against the reference's wrapped samples (x in [31, 33), z in
+// [62, 64)). on = false, or a condition failing: no clause (+inf / -inf, nothing resolved early).
+static void early_geo_setup(const SceneGeo& g, int light_pos, bool on, KParams* K) {
+  for (int b = 0; b < 2; ++b) {
+    K->eb_top[b] = INFINITY; K->eb_sgn[b] = 1.0f; K->eb_bnd[b] = -INFINITY; K->eb_z[b] = 0;
+  }
+  for (int a = 0; a < 3; ++a) K->er_lo[a] = K->er_span[a] = 0;
+  bool ok = on && g.has_room && g.n_box == 2 && light_pos >= 0 && light_pos < g.n_xy + g.n_xz + g.n_yz &&
+            light_pos >= g.n_xy && light_pos < g.n_xy + g.n_xz;  // an XZ light
+  if (!ok) return;
+  const int nt = g.n_txy + g.n_txz + g.n_tyz;
+  float lo[3], hi[3];
+  for (int a = 0; a < 3; ++a) {  // room tests: XY pair (planes z), XZ (y), YZ (x)
+    const GeoTest& R = g.test[nt + a];
+    const int ax = a == 0 ? 2 : (a == 1 ? 1 : 0);
+    lo[ax] = std::min(R.k0, R.k1);
+    hi[ax] = std::max(R.k0, R.k1);
+    ok = ok && lo[ax] >= 0.0f && hi[ax] - lo[ax] <= 1000.0f;
+  }
+  const GeoRect& L = g.rect[light_pos];
+  const float yl = L.k;
+  ok = ok && L.ha >= 0.0f && L.hb >= 0.0f && L.ma - L.ha >= lo[0] + 1.0f && L.ma + L.ha <= hi[0] - 1.0f &&
+       L.mb - L.hb >= lo[2] + 1.0f && L.mb + L.hb <= hi[2] - 1.0f && yl >= lo[1] + 1.0f && yl <= 81.5f &&
+       hi[1] >= yl + 0.05f;
+  for (int b = 0; ok && b < 2; ++b) {
+    const GeoTest &XY = g.test[nt + 3 + 3 * b], &YZ = g.test[nt + 4 + 3 * b], &T = g.test[nt + 5 + 3 * b];
+    const float z0 = std::min(XY.k0, XY.k1), z1 = std::max(XY.k0, XY.k1);
+    const float x0 = std::min(YZ.k0, YZ.k1), x1 = std::max(YZ.k0, YZ.k1);
+    // the box top at least 0.5 below the light plane (a top just under the plane left
+    // the box's y-slab exit within rounding of the light crossing)
+    if (!(T.k0 <= yl - 0.5f)) { ok = false; break; }
+    K->eb_top[b] = T.k0;
+    if (x0 >= 33.0f) { K->eb_sgn[b] = 1.0f; K->eb_bnd[b] = x0; K->eb_z[b] = 0; }
+    else if (x1 <= 31.0f) { K->eb_sgn[b] = -1.0f; K->eb_bnd[b] = -x1; K->eb_z[b] = 0; }
+    else if (z0 >= 64.0f) { K->eb_sgn[b] = 1.0f; K->eb_bnd[b] = z0; K->eb_z[b] = 1; }
+    else if (z1 <= 62.0f) { K->eb_sgn[b] = -1.0f; K->eb_bnd[b] = -z1; K->eb_z[b] = 1; }
+  }
+  if (!ok) {
+    for (int b = 0; b < 2; ++b) { K->eb_top[b] = INFINITY; K->eb_sgn[b] = 1.0f; K->eb_bnd[b] = -INFINITY; }
+    return;
+  }
+  for (int a = 0; a < 3; ++a) {
+    const float top = a == 1 ? std::nextafter(yl, 0.0f) : hi[a];  // y < y_L
+    uint32_t blo, btop;
+    std::memcpy(&blo, &lo[a], 4);
+    std::memcpy(&btop, &top, 4);
+    K->er_lo[a] = blo;
+    K->er_span[a] = btop - blo;
+  }
+}
+
 extern "C" spt_status spt_context_create(int32_t device, spt_context** out) {
   if (!out) return fail(SPT_ERR_INVALID_ARG, "null out");
   int count = 0;
@@ -2201,6 +2347,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // (each estimator kernel in two forms: the leak-end rule, or leaked paths as the reference's)
   const bool ref_est = K.light_black && p->max_depth == 0 && p->rr_depth >= 1 && cam_axis && lref;
   const bool head_est = cconst && kcap >= 3 && ref_est;
+  // any other camera (finite): the literal kernels' CAMAX 2 forms (round 6; leak-end rule only)
+  bool cam_fin = true;
+  for (int i = 0; i < 12; ++i) cam_fin = cam_fin && std::isfinite(K.cam[i]);
+  const bool ref_est_cam = K.light_black && p->max_depth == 0 && p->rr_depth >= 1 && cam_fin && lref &&
+                           !cam_axis && K.leak_end;
+  const bool head_est_cam = cconst && kcap >= 3 && ref_est_cam;
+  const bool upbox_cam = cornell && !cconst && kcap >= 3 && ref_est_cam && cornell_room_match(g);
+  const bool wrap_nee = p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP;
   // the HEAD topology with uploaded geometry (an edited rect[]: a box moved, a wall resized) and
   // the reference's estimator: geometry from LDS, the estimator's branches compile-time
   const bool cornell_est = cornell && !cconst && kcap >= 2 && ref_est && K.leak_end;
@@ -2208,7 +2362,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   if (head_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP)
     kv = K.leak_end ? KV_CONST_NEE : KV_CONST_NEE_REF;
   else if (head_est && p->nee_prob <= 0.0f) kv = K.leak_end ? KV_CONST_COS : KV_CONST_COS_REF;
+  else if (head_est_cam && wrap_nee) kv = KV_CONST_NEE_CAM;
+  else if (head_est_cam && p->nee_prob <= 0.0f) kv = KV_CONST_COS_CAM;
   else if (cconst) kv = KV_CONST;
+  else if (upbox_cam && wrap_nee) kv = KV_UPBOX_NEE_CAM;
+  else if (upbox_cam && p->nee_prob <= 0.0f) kv = KV_UPBOX_COS_CAM;
   else if (cornell_est && p->nee_prob >= 1.0f && p->light_mode == SPT_LIGHT_GLIBC_WRAP) kv = KV_CORNELL_NEE;
   else if (cornell_est && p->nee_prob <= 0.0f) kv = KV_CORNELL_COS;
   else if (cornell) kv = KV_CORNELL;
@@ -2226,13 +2384,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                  prims[p->light_id].kind == SPT_RECT_XZ
              ? (K.leak_end ? KV_SPHDIFF_NEE : KV_SPHDIFF_NEE_REF)
              : KV_SPHDIFF;
-  if (kv == KV_CORNELL_COS && kcap >= 3 && n_prims >= 7) {  // the cosine estimator: no clauses needed
-    spt_prim head[17];
-    int32_t nh = 0;
-    bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
-    for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
-    if (ok) kv = KV_UPBOX_COS;  // the room and light HEAD's: only the boxes uploaded
-  }
+  if (kv == KV_CORNELL_COS && kcap >= 3 && cornell_room_match(g))
+    kv = KV_UPBOX_COS;  // the room HEAD's: the room literal, the light and the boxes uploaded
   // The sphere NEE kernel's early resolve needs the HEAD room (rect[] :287-294, light at index 6)
   // as prims 0..6, nothing else but narrow spheres, and a threshold above every sphere's top
   // (early_room_proven); otherwise it stays off (+inf) and every shadow ray is traced.
@@ -2262,36 +2415,13 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
       K.early_y0 = y0;
     }
   }
-  // The uploaded-geometry HEAD-topology NEE kernel's early resolve (early_geo_proven): the HEAD
-  // room and light (prims 0..6 bit-equal to :288-294) and two boxes below the light plane; per box
-  // the clause the reference's wrapped light samples allow (oracle c_find_early_clauses). Anything
-  // else: no clause, nothing resolved early.
-  for (int b = 0; b < 2; ++b) {
-    K.eb_top[b] = INFINITY; K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = -INFINITY; K.eb_z[b] = 0;
-  }
-  if (kv == KV_CORNELL_NEE && g.n_box == 2 && n_prims >= 7) {
-    spt_prim head[17];
-    int32_t nh = 0;
-    bool ok = spt_scene_cornell(head, 17, &nh) == SPT_OK;
-    for (int i = 0; ok && i < 7; ++i) ok = std::memcmp(&prims[i], &head[i], sizeof(spt_prim)) == 0;
-    // the room and light are HEAD's: at the auto level the boxes-only-uploaded kernel (the room,
-    // the light and the estimator literal); the const level keeps the uploaded-geometry kernel
-    if (ok && kcap >= 3) kv = KV_UPBOX_NEE;
-    const int nt = g.n_txy + g.n_txz + g.n_tyz;
-    for (int b = 0; ok && b < 2; ++b) {
-      const GeoTest &XY = g.test[nt + 3 + 3 * b], &YZ = g.test[nt + 4 + 3 * b], &T = g.test[nt + 5 + 3 * b];
-      const float z0 = std::min(XY.k0, XY.k1), z1 = std::max(XY.k0, XY.k1);
-      const float x0 = std::min(YZ.k0, YZ.k1), x1 = std::max(YZ.k0, YZ.k1);
-      if (!(T.k0 < 81.5f)) { ok = false; break; }
-      K.eb_top[b] = T.k0;
-      if (x0 >= 33.0f) { K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = x0; K.eb_z[b] = 0; }
-      else if (x1 <= 31.0f) { K.eb_sgn[b] = -1.0f; K.eb_bnd[b] = -x1; K.eb_z[b] = 0; }
-      else if (z0 >= 64.0f) { K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = z0; K.eb_z[b] = 1; }
-      else if (z1 <= 62.0f) { K.eb_sgn[b] = -1.0f; K.eb_bnd[b] = -z1; K.eb_z[b] = 1; }
-    }
-    if (!ok)
-      for (int b = 0; b < 2; ++b) { K.eb_top[b] = INFINITY; K.eb_sgn[b] = 1.0f; K.eb_bnd[b] = -INFINITY; }
-  }
+  // The uploaded-geometry HEAD-topology NEE kernel's early resolve (early_geo_proven): the room,
+  // the light and two boxes with the margins early_geo_setup checks, the clauses it picks (oracle
+  // c_find_early_clauses). Anything else: no clause, nothing resolved early.
+  early_geo_setup(g, light_pos, kv == KV_CORNELL_NEE || kv == KV_UPBOX_NEE_CAM, &K);
+  // the room HEAD's: at the auto level the kernel with the room literal (the light, the boxes and
+  // the estimator's constants uploaded / literal); the const level keeps the uploaded-geometry one
+  if (kv == KV_CORNELL_NEE && kcap >= 3 && cornell_room_match(g)) kv = KV_UPBOX_NEE;
   // Unit size: SPT_UNITS_PER_LANE (8) units per resident lane (C3: 96 samples); never changes
   // results (integer accumulation). Round 1 chose 16 (25.0 ms vs 26.0 ms at 8 units/lane, before
   // in-wave stealing); re-measured in round 4 with stealing, unit slots and two frames in flight
@@ -2345,7 +2475,9 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // the literal HEAD NEE kernels (and the boxes-only-uploaded one: edited scene -4 %) at 8 blocks
   // per CU only (the measured shape): the sphere kernel (C5) lost 3.6 %, the uploaded-geometry
   // kernels 0.5-2.4 % of kernel time or ~1.5 % of pipelined value (profiles/r05_young_cut_ab.json)
-  if (!small_launch && bpc == 8 && (kv == KV_CONST_NEE || kv == KV_CONST_NEE_REF || kv == KV_UPBOX_NEE) &&
+  if (!small_launch && bpc == 8 &&
+      (kv == KV_CONST_NEE || kv == KV_CONST_NEE_REF || kv == KV_UPBOX_NEE || kv == KV_CONST_NEE_CAM ||
+       kv == KV_UPBOX_NEE_CAM) &&
       SPT_YOUNG_CUT > 0) {
     K.young_block = (uint32_t)(SPT_YOUNG_RANK * c->n_cu);
     K.young_cut = (uint32_t)(n_units * (uint64_t)SPT_YOUNG_CUT / 1000u);
@@ -2413,7 +2545,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 #ifdef SPT_WAVE_TIMES
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
-  c->nee_by_identity = kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
+  c->nee_by_identity = kv == KV_CONST_NEE_CAM || kv == KV_UPBOX_NEE_CAM ||
+                       kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
                        kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE || kv == KV_RECTDIFF_NEE ||
                        kv == KV_UPBOX_NEE;
   const int grid = c->n_cu * bpc;

@@ -128,16 +128,30 @@ def test_every_kernel_specialisation_bit_exact(spt, oracle, kernel, est, q, fl):
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
 
 
+TILTED = dict(lookfrom=(40, 55, 160), lookat=(55, 35, 10), vup=(0.1, 1, 0))
+
+
+@pytest.mark.parametrize("scene", ["head", "edited"])
+@pytest.mark.parametrize("flags", [0, 4, 2 << 8])
 @pytest.mark.parametrize("est,q", [("nee", 1.0), ("cos", 0.0)])
-def test_tilted_camera_leaves_the_axis_aligned_specialisation(spt, oracle, est, q):
-    """A camera whose horizontal/vertical vectors are not axis-aligned takes the run-time camera
-    form (Cfg CAMAX only holds for the reference's :521 camera): same contract, same bits."""
-    p = spt.default_params(width=48, height=36, spp=8, seed=17, nee_prob=q)
-    cam = spt.Camera(lookfrom=(40, 55, 160), lookat=(55, 35, 10), vup=(0.1, 1, 0), aspect=48 / 36)
-    gpu, gst = spt.render(spt.cornell_scene(), cam, p, return_stats=True)
-    cpu, cst = oracle.counter_render(spt.cornell_scene(), cam._c, p)
+def test_tilted_camera_bit_exact(spt, oracle, est, q, flags, scene):
+    """A camera whose horizontal/vertical vectors are not axis-aligned (Camera :262-275 with another
+    lookat and vup). Round 6: the literal kernels' any-camera forms (Cfg CAMAX 2: KV_CONST_*_CAM on
+    the HEAD scene, KV_UPBOX_*_CAM on an edited one with the HEAD room) keep the early shadow-ray
+    resolve; flags 4 (the reference's leaks) and the cornell cap (2 << 8) take the run-time camera
+    kernels. Same contract, same bits, and (NEE, auto) shadow rays resolved without a trace."""
+    import test_oracle as to
+
+    prims = (spt.cornell_scene() if scene == "head" else
+             to.edited_scene(spt, **to.EDITS_LR[1][0]))
+    p = spt.default_params(width=48, height=36, spp=8, seed=17, nee_prob=q, flags=flags)
+    cam = spt.Camera(aspect=48 / 36, **TILTED)
+    gpu, gst = spt.render(prims, cam, p, return_stats=True)
+    cpu, cst = oracle.counter_render(prims, cam._c, p)
     _assert_exact(gpu, cpu)
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    if est == "nee":
+        assert (gst["shadow_proven"] > 0) == (flags == 0), gst["shadow_proven"]
 
 
 def test_specialisation_needs_all_diff(spt, oracle):
@@ -544,8 +558,8 @@ def test_reference_leaks_flag_bit_exact(spt, oracle, kernel, nee):
 
 
 def test_reference_leaks_c3_rows_bit_exact(spt, oracle):
-    """C3's size and spp with SPT_FLAG_REFERENCE_LEAKS, on a spread subset of its rows (the leftover
-    launch and the reference-leak HEAD NEE kernel at full size)."""
+    """C3's size and spp with SPT_FLAG_REFERENCE_LEAKS, on a spread subset of its rows (the
+    reference-leak HEAD NEE kernel at full size: unit slots, stealing and the young-block cut)."""
     p = spt.default_params(width=1024, height=768, spp=512, seed=1, flags=spt.FLAG_REFERENCE_LEAKS)
     cam = spt.Camera(aspect=float(np.float32(1024) / np.float32(768)))
     gpu = spt.render(spt.cornell_scene(), cam, p)
@@ -624,3 +638,41 @@ def test_edited_scene_early_resolve_matches_oracle_proof(spt, oracle, edit, kern
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
     assert bad == 0 and claims > 0, (claims, bad)
     assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "const"])
+@pytest.mark.parametrize("edit", range(9))
+def test_edited_light_and_room_early_resolve_matches_oracle_proof(spt, oracle, edit, kernel):
+    """Round 6: the light and the room edited as well (test_oracle.EDITS_LR). auto: the room HEAD's
+    -> the room-literal kernel with the light and boxes from LDS (KV_UPBOX_NEE), else the
+    uploaded-geometry one (KV_CORNELL_NEE); const: KV_CORNELL_NEE. Bit-exact image and statistics,
+    and the shadow rays resolved without a trace are exactly the oracle's claims (none where the
+    scene is outside the clause margins)."""
+    import test_oracle as to
+
+    kw, on = to.EDITS_LR[edit]
+    prims = to.edited_scene(spt, **kw)
+    p = spt.default_params(width=96, height=72, spp=16, seed=40 + edit, flags=spt.kernel_flag(kernel))
+    oracle.proof_check(True, edited=True)
+    try:
+        gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert bad == 0 and (claims > 0) == on, (claims, bad)
+    assert gst["shadow_proven"] == claims, (gst["shadow_proven"], claims)
+
+
+@pytest.mark.parametrize("edit", [0, 1, 3])
+def test_edited_light_cosine_bit_exact(spt, oracle, edit):
+    """The cosine-only estimator on an edited light / room (KV_UPBOX_COS when the room is HEAD's,
+    KV_CORNELL_COS otherwise): equal to the oracle."""
+    import test_oracle as to
+
+    prims = to.edited_scene(spt, **to.EDITS_LR[edit][0])
+    p = spt.default_params(width=64, height=48, spp=16, seed=9, nee_prob=0.0)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst

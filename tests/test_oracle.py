@@ -507,3 +507,63 @@ def test_early_nee_resolve_proof_holds_edited_geometry(oracle, spt, edit):
         oracle.proof_check(False)
     assert bad == 0, (claims, bad)
     assert claims > 0.3 * st["nee_light_hits"], (claims, st["nee_light_hits"])
+
+
+def _tall_box_height(spt, prims, hgt):
+    """rect[] with the tall box (prims 7-11) raised to height hgt."""
+    out = [spt.spt_prim.from_buffer_copy(p) for p in prims]
+    for i in (7, 8):   # XY faces: y bounds geom[2:4]
+        out[i].geom[3] = hgt
+    for i in (9, 10):  # YZ faces: y bounds geom[0:2]
+        out[i].geom[1] = hgt
+    out[11].geom[4] = hgt
+    return out
+
+
+# Round 6: edits of the light and the room (early_geo_setup / c_find_early_clauses). on = whether
+# the scene meets the clause conditions (a light plane 0.02 under the ceiling, a box top 0.3 under
+# the light plane, a light 0.5 from a wall: no clause, nothing resolved early, still exact).
+EDITS_LR = [
+    (dict(light=dict(x=(30, 66), z=(65, 99))), True),
+    (dict(light=dict(x=(28, 72), z=(60, 100), y=80.0, e=15)), True),
+    (dict(room=dict(depth=150.0, width=(2.0, 98.0))), True),
+    (dict(room=dict(height=90.0), light=dict(y=81.0)), True),
+    (dict(room=dict(depth=160.0), light=dict(x=(30, 70), y=81.0), short=(-20.0, 0.0)), True),
+    (dict(light=dict(y=81.58)), False),
+    (dict(tall=81.2), False),
+    (dict(tall=80.9), True),
+    (dict(light=dict(x=(1.5, 40))), False),
+]
+
+
+def edited_scene(spt, light=None, room=None, short=(0.0, 0.0), tall=None):
+    prims = _move_boxes(spt, short=short)
+    if tall is not None:
+        prims = _tall_box_height(spt, prims, tall)
+    if room is not None:
+        prims = spt.edit_room(prims, **room)
+    if light is not None:
+        prims = spt.edit_light(prims, **light)
+    return prims
+
+
+@pytest.mark.parametrize("edit", range(len(EDITS_LR)))
+def test_early_nee_resolve_proof_holds_edited_light_and_room(oracle, spt, edit):
+    """The early resolve of an edited rect[] whose light or room moved as well (round 6): the room
+    clause from the room's own box and the light plane, the box clauses as before. No claim is
+    contradicted by the contract's intersect, and a scene outside the margins gets no claim."""
+    kw, on = EDITS_LR[edit]
+    prims = edited_scene(spt, **kw)
+    p = oracle.default_params(width=128, height=96, spp=24, seed=17 + edit)
+    assert oracle.scene_boxes(prims, p) == 2
+    oracle.proof_check(True, edited=True)
+    try:
+        _, st = oracle.counter_render(prims, oracle.camera(128 / 96), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    assert bad == 0, (claims, bad)
+    if on:
+        assert claims > 0.3 * st["nee_light_hits"], (claims, st["nee_light_hits"])
+    else:
+        assert claims == 0 and st["nee_light_hits"] > 0, (claims, st["nee_light_hits"])
