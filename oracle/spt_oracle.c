@@ -1137,6 +1137,31 @@ static int c_early_nee_proven(const c_ctx* C, fv o, fv d, float* tl) {
   }
   return acc && room && short_box && tall_box;
 }
+/* Test hook (the shadow-ray slot model): the light-accepted shadow rays that the HEAD
+ * early resolve leaves to a trace (proof mode 1), by outcome and by why the predicate failed.
+ *  [0] reached the light  [1] blocked
+ *  [2] reached, vertex outside the room box (rounded through its wall)  [3] blocked, same
+ *  [4] blocked by the vertex's own primitive (a self-hit)  [5] blocked, own prim, vertex outside
+ *  [6] reached, short-box clause failed (tall ok)  [7] reached, tall failed (short ok)  [8] both
+ *  [9] blocked, vertex's own axis coordinate outside the room's range, all others inside */
+static uint64_t g_census[16];
+static void c_shadow_census(const c_ctx* C, fv o, fv d, int vid, int hid) {
+  const int reached = hid == C->P->light_id;
+  const int room = asu(o.x) - asu(1.0f) <= asu(99.0f) - asu(1.0f) && asu(o.z) <= asu(170.0f) &&
+                   asu(o.y) < asu(81.5f);
+  const int short_box = o.y >= 25.0f || o.x <= 63.0f, tall_box = o.y >= 50.0f || o.z >= 62.0f;
+  (void)d;
+  __atomic_fetch_add(&g_census[reached ? 0 : 1], 1, __ATOMIC_RELAXED);
+  if (!room) __atomic_fetch_add(&g_census[reached ? 2 : 3], 1, __ATOMIC_RELAXED);
+  if (!reached && hid == vid) __atomic_fetch_add(&g_census[room ? 4 : 5], 1, __ATOMIC_RELAXED);
+  if (reached && room)
+    __atomic_fetch_add(&g_census[!short_box && tall_box ? 6 : (short_box && !tall_box ? 7 : 8)], 1,
+                       __ATOMIC_RELAXED);
+}
+void spt_oracle_shadow_census(uint64_t out[16]) {
+  int i;
+  for (i = 0; i < 16; i++) { out[i] = g_census[i]; g_census[i] = 0; }
+}
 void spt_oracle_proof_check(int on, float y0) {
   g_proof_on = on;
   g_proof_y0 = y0;
@@ -1576,6 +1601,8 @@ static fv c_path(const c_ctx* C, uint32_t pix, uint32_t s, int px, int py, const
             __atomic_fetch_add(&g_proof_n, 1, __ATOMIC_RELAXED);
             if (!sh || ids != P->light_id || asu(ts) != asu(tl))
               __atomic_fetch_add(&g_proof_bad, 1, __ATOMIC_RELAXED);
+          } else if (g_proof_on == 1 && c_light_accepts(C, x, dl)) {
+            c_shadow_census(C, x, dl, id, sh ? ids : -1);
           }
         }
         st->nee_events++;

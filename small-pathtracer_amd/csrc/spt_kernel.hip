@@ -224,6 +224,7 @@ struct KParams {  // in device memory, read through a laundered constant-space p
   // per axis (bits(v) - er_lo) <= er_span on the float bits (HEAD: x in [1, 99], y in [0, 81.5),
   // z in [0, 170], the literal early_room_ok); er_lo = 0, er_span = 0 with no clause
   uint32_t er_lo[3], er_span[3];
+  uint32_t ul_ybits;  // the room-literal light-uploaded kernel's y bound: bits(y) < bits(y_L)
   int unit_dirs;  // oracle c_unit_dirs: the scene has a sphere or a REFR primitive
   float nee_c;    // light_area / pi rounded once (the free-scale NEE weight, nee_weight)
   unsigned long long* accum;  // [n_local_pix][3] 1.31 fixed point (stolen ranges; every unit without slots)
@@ -256,13 +257,16 @@ struct CornellRectPtr {
 // NT*: rect tests per kind (parallel pairs count once).
 template <int NXY_, int NXZ_, int NYZ_, bool SPH_, int LPOS_, bool CONSTGEO_ = false,
           int NTXY_ = -1, int NTXZ_ = -1, int NTYZ_ = -1, bool MAT_ = SPH_, bool WIDE_ = false,
-          int NBOX_ = -1, bool UPBOX_ = false>
+          int NBOX_ = -1, bool UPBOX_ = false, bool UPLIGHT_ = false>
 struct Topo {
   static constexpr int NBOX = NBOX_;  // boxes of contract v6 (uploaded geometry; -1 = run time)
   // CONSTGEO with the two boxes uploaded (an edited rect[] whose room and light are HEAD's): the
   // room and light as literals, the boxes' slab tests from LDS, the early resolve's box clauses
   // from KParams (early_geo_proven)
   static constexpr bool UPBOX = UPBOX_;
+  // UPBOX with the light uploaded as well (an edited light; the room literal): the light's test from
+  // the uploaded scene through scalar loads, its plane's y bound of the early resolve from KParams
+  static constexpr bool UPLIGHT = UPLIGHT_;
   static constexpr int NXY = NXY_, NXZ = NXZ_, NYZ = NYZ_, LPOS = LPOS_;
   static constexpr int NTXY = NTXY_, NTXZ = NTXZ_, NTYZ = NTYZ_;
   static constexpr bool SPH = SPH_, CONSTGEO = CONSTGEO_, MAT = MAT_;
@@ -279,6 +283,9 @@ using TopoCornellConst = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCor
 // the same with the boxes uploaded (a box moved or resized; room, light and topology HEAD's)
 using TopoCornellUpBox = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true, -1, -1,
                               -1, false, false, 2, true>;
+// ... and with the light uploaded too (the light moved or resized; the room HEAD's)
+using TopoCornellUpLight = Topo<kCornellNXY, kCornellNXZ, kCornellNYZ, false, kCornellLightPos, true, -1, -1,
+                                -1, false, false, 2, true, true>;
 using TopoGeneric = Topo<-1, -1, -1, true, -1>;
 // Any scene with spheres but only DIFF materials and cosine scattering (the C5 32-sphere scene):
 // no SPEC/REFR stack and branch words, 8 waves/SIMD instead of the generic kernel's 6.
@@ -646,8 +653,10 @@ __device__ __forceinline__ bool intersect_scene(const SPT_CONST SceneGeo* G, GP 
     if constexpr (TP::UPBOX) {
       // the uploaded HEAD-topology tests (host-checked: n_txy 0, n_txz 1, n_tyz 0): the light, the
       // room's three pairs (its XZ pair's k0 the floor), then the two boxes' three tests each. The
-      // room is literal (HEAD's, host-checked); the light and the boxes come from LDS.
-      light_cand(tests[0], rays[1], tmin);
+      // room is literal (HEAD's, host-checked), the boxes come from LDS, the light is literal or
+      // (UPLIGHT) read through scalar loads from the uploaded scene
+      if constexpr (TP::UPLIGHT) light_cand(G->test[0], rays[1], tmin);
+      else cornell_tests(std::make_integer_sequence<int, kCornellTests.n>{}, rays, tmin);  // the light
       geo_box(tests + 4, tests + 2, rays[2], rays[1], rays[0], tmin);
       geo_box(tests + 7, tests + 2, rays[2], rays[1], rays[0], tmin);
     } else {
@@ -816,8 +825,20 @@ __device__ __forceinline__ int early_room_ok_k(f3 x, const SPT_CONST KParams* P)
          (int)(__float_as_uint(x.y) - P->er_lo[1] <= P->er_span[1]) &
          (int)(__float_as_uint(x.z) - P->er_lo[2] <= P->er_span[2]);
 }
+// ROOM: 0 = the literal HEAD room and light plane (early_room_ok; the boxes-only-uploaded kernels),
+// 1 = the literal room with the light plane's bound from KParams (UPLIGHT), 2 = everything from
+// KParams (the uploaded-geometry kernels)
+template <int ROOM>
 __device__ __forceinline__ bool early_geo_proven(f3 x, const SPT_CONST KParams* P) {
-  int ok = early_room_ok_k(x, P);
+  int ok;
+  if constexpr (ROOM == 0) {
+    ok = early_room_ok(x);
+  } else if constexpr (ROOM == 1) {
+    ok = (int)(__float_as_uint(x.x) - __float_as_uint(1.0f) <= __float_as_uint(99.0f) - __float_as_uint(1.0f)) &
+         (int)(__float_as_uint(x.z) <= __float_as_uint(170.0f)) & (int)(__float_as_uint(x.y) < P->ul_ybits);
+  } else {
+    ok = early_room_ok_k(x, P);
+  }
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const float v = P->eb_z[b] ? x.z : x.x;
@@ -1237,7 +1258,7 @@ render_kernel(const KParams* __restrict__ Pg) {
 #ifdef SPT_PROBE_VALU  // diagnostic build SPT_DIAG=4: N extra VALU per wave-iteration
       { float z_ = o.x; asm volatile(".rept " SPT_XSTR(SPT_PROBE_VALU) "\n v_add_f32 %0, 1.0, %0\n .endr" : "+v"(z_)); }
 #endif
-      const SPT_CONST SceneGeo* G = TP::CONSTGEO ? nullptr : cptr(P->geo);
+      const SPT_CONST SceneGeo* G = TP::CONSTGEO && !TP::UPLIGHT ? nullptr : cptr(P->geo);
       // intersect() leaves id untouched on a miss (:323-335): a shadow ray keeps its vertex's id. The
       // early-resolve HEAD kernel needs no vertex id: its light is black, so no vertex on the light
       // takes a NEE sample, and a missed shadow ray's id (prim 0's) is not the light's either way.
@@ -1472,10 +1493,11 @@ render_kernel(const KParams* __restrict__ Pg) {
             if constexpr (kEarlyNee) {  // the light's own test (light_accepts), keeping t and a
               const Ray6 rl6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z};
               RectHit h;
-              if constexpr (TP::UPBOX) h = rect_eval_test(s_test[0], rl6);  // the uploaded light
+              if constexpr (TP::UPLIGHT) h = rect_eval_test(cptr(D->geo)->test[0], rl6);  // the uploaded light
               else h = rect_eval(CornellRectPtr{kCornellLightPos}, rl6);
               la = h.inb & key_valid(h.tt, kCornellLightPos);
-              if constexpr (TP::UPBOX) early = la & early_geo_proven(x, D);
+              if constexpr (TP::UPLIGHT) early = la & early_geo_proven<1>(x, D);
+              else if constexpr (TP::UPBOX) early = la & early_geo_proven<0>(x, D);
               else early = la & early_nee_proven(x);
               // The weight of :471-472 now, for a proven lane and a traced one alike: nee_weight's
               // arithmetic with |dl . nl| = |dl_a| on the normal's axis a (the dot's zero terms are
@@ -1490,7 +1512,7 @@ render_kernel(const KParams* __restrict__ Pg) {
                                           Ray6{x.y, rcp_nr(dl.y), dl.x, x.x, dl.z, x.z});
               la = h.inb & key_valid(h.tt, (uint32_t)D->light_pos);
               if constexpr (kEarlySph) early = la & early_room_proven(x, D->early_y0);
-              else early = la & early_geo_proven(x, D);
+              else early = la & early_geo_proven<2>(x, D);
               t = early ? h.tt : t;
             } else {
               la = light_accepts<TP>(D, G2, rects_of<TP>(G2), x, dl);
@@ -1732,7 +1754,8 @@ using RenderFn = void (*)(const KParams*);
 enum { KV_GENERIC, KV_CORNELL, KV_CONST, KV_CONST_NEE, KV_CONST_COS, KV_SPHDIFF, KV_WIDE,
        KV_SPHDIFF_NEE, KV_RECTDIFF, KV_CONST_NEE_REF, KV_CONST_COS_REF, KV_SPHDIFF_NEE_REF,
        KV_CORNELL_NEE, KV_CORNELL_COS, KV_RECTDIFF_NEE, KV_RECTDIFF_COS, KV_UPBOX_NEE, KV_UPBOX_COS,
-       KV_CONST_NEE_CAM, KV_CONST_COS_CAM, KV_UPBOX_NEE_CAM, KV_UPBOX_COS_CAM, KV_COUNT };
+       KV_CONST_NEE_CAM, KV_CONST_COS_CAM, KV_UPBOX_NEE_CAM, KV_UPBOX_COS_CAM, KV_UPLIGHT_NEE,
+       KV_UPLIGHT_COS, KV_UPLIGHT_NEE_CAM, KV_UPLIGHT_COS_CAM, KV_COUNT };
 static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoGeneric, CfgRuntime>, render_kernel<TopoCornell, CfgRuntime>,
     render_kernel<TopoCornellConst, CfgRuntime>, render_kernel<TopoCornellConst, CfgHeadNee>,
@@ -1744,7 +1767,9 @@ static const RenderFn kRenderKernels[KV_COUNT] = {
     render_kernel<TopoRectDiff, CfgHeadNee>, render_kernel<TopoRectDiff, CfgHeadCos>,
     render_kernel<TopoCornellUpBox, CfgHeadNee>, render_kernel<TopoCornellUpBox, CfgHeadCos>,
     render_kernel<TopoCornellConst, CfgHeadNeeCam>, render_kernel<TopoCornellConst, CfgHeadCosCam>,
-    render_kernel<TopoCornellUpBox, CfgHeadNeeCam>, render_kernel<TopoCornellUpBox, CfgHeadCosCam>};
+    render_kernel<TopoCornellUpBox, CfgHeadNeeCam>, render_kernel<TopoCornellUpBox, CfgHeadCosCam>,
+    render_kernel<TopoCornellUpLight, CfgHeadNee>, render_kernel<TopoCornellUpLight, CfgHeadCos>,
+    render_kernel<TopoCornellUpLight, CfgHeadNeeCam>, render_kernel<TopoCornellUpLight, CfgHeadCosCam>};
 
 struct spt_context {
   int device = 0;
@@ -2121,6 +2146,16 @@ static bool cornell_room_match(const SceneGeo& g) {
   return true;
 }
 
+// The light of a HEAD-room scene is the reference's (:294, fp32 geometry at grouped position 8): the
+// boxes-only-uploaded kernels keep it literal, the UPLIGHT ones read it from the uploaded scene.
+static bool cornell_light_match(const SceneGeo& g, int light_pos) {
+  if (light_pos != kCornellLightPos) return false;
+  const GeoRect& R = g.rect[light_pos];
+  const CRect& H = kCornellRects[light_pos];
+  const float a[5] = {R.k, R.ma, R.ha, R.mb, R.hb}, b[5] = {H.k, H.ma, H.ha, H.mb, H.hb};
+  return std::memcmp(a, b, sizeof a) == 0 && R.idx == H.idx;
+}
+
 // The early resolve's clauses for a HEAD-topology scene with the reference's estimator (oracle
 // c_find_early_clauses, which the proof tests check claim by claim): the room's box with y below
 // the light plane (early_room_ok_k), the light's rectangle >= 1 inside the side walls and >= 1 above
@@ -2384,8 +2419,11 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
                  prims[p->light_id].kind == SPT_RECT_XZ
              ? (K.leak_end ? KV_SPHDIFF_NEE : KV_SPHDIFF_NEE_REF)
              : KV_SPHDIFF;
-  if (kv == KV_CORNELL_COS && kcap >= 3 && cornell_room_match(g))
-    kv = KV_UPBOX_COS;  // the room HEAD's: the room literal, the light and the boxes uploaded
+  // the room HEAD's: the room literal, the boxes uploaded, the light literal when it is HEAD's too
+  const bool light_head = cornell_light_match(g, light_pos);
+  if (kv == KV_CORNELL_COS && kcap >= 3 && cornell_room_match(g)) kv = light_head ? KV_UPBOX_COS : KV_UPLIGHT_COS;
+  if (kv == KV_UPBOX_NEE_CAM && !light_head) kv = KV_UPLIGHT_NEE_CAM;
+  if (kv == KV_UPBOX_COS_CAM && !light_head) kv = KV_UPLIGHT_COS_CAM;
   // The sphere NEE kernel's early resolve needs the HEAD room (rect[] :287-294, light at index 6)
   // as prims 0..6, nothing else but narrow spheres, and a threshold above every sphere's top
   // (early_room_proven); otherwise it stays off (+inf) and every shadow ray is traced.
@@ -2418,10 +2456,14 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // The uploaded-geometry HEAD-topology NEE kernel's early resolve (early_geo_proven): the room,
   // the light and two boxes with the margins early_geo_setup checks, the clauses it picks (oracle
   // c_find_early_clauses). Anything else: no clause, nothing resolved early.
-  early_geo_setup(g, light_pos, kv == KV_CORNELL_NEE || kv == KV_UPBOX_NEE_CAM, &K);
+  early_geo_setup(g, light_pos, kv == KV_CORNELL_NEE || kv == KV_UPBOX_NEE_CAM || kv == KV_UPLIGHT_NEE_CAM, &K);
+  {
+    const float yl = light_pos >= 0 ? g.rect[light_pos].k : 0.0f;
+    std::memcpy(&K.ul_ybits, &yl, 4);
+  }
   // the room HEAD's: at the auto level the kernel with the room literal (the light, the boxes and
   // the estimator's constants uploaded / literal); the const level keeps the uploaded-geometry one
-  if (kv == KV_CORNELL_NEE && kcap >= 3 && cornell_room_match(g)) kv = KV_UPBOX_NEE;
+  if (kv == KV_CORNELL_NEE && kcap >= 3 && cornell_room_match(g)) kv = light_head ? KV_UPBOX_NEE : KV_UPLIGHT_NEE;
   // Unit size: SPT_UNITS_PER_LANE (8) units per resident lane (C3: 96 samples); never changes
   // results (integer accumulation). Round 1 chose 16 (25.0 ms vs 26.0 ms at 8 units/lane, before
   // in-wave stealing); re-measured in round 4 with stealing, unit slots and two frames in flight
@@ -2477,7 +2519,7 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
   // kernels 0.5-2.4 % of kernel time or ~1.5 % of pipelined value (profiles/r05_young_cut_ab.json)
   if (!small_launch && bpc == 8 &&
       (kv == KV_CONST_NEE || kv == KV_CONST_NEE_REF || kv == KV_UPBOX_NEE || kv == KV_CONST_NEE_CAM ||
-       kv == KV_UPBOX_NEE_CAM) &&
+       kv == KV_UPBOX_NEE_CAM || kv == KV_UPLIGHT_NEE || kv == KV_UPLIGHT_NEE_CAM) &&
       SPT_YOUNG_CUT > 0) {
     K.young_block = (uint32_t)(SPT_YOUNG_RANK * c->n_cu);
     K.young_cut = (uint32_t)(n_units * (uint64_t)SPT_YOUNG_CUT / 1000u);
@@ -2545,7 +2587,8 @@ extern "C" spt_status spt_render_async(spt_context* c, const spt_prim* prims, in
 #ifdef SPT_WAVE_TIMES
   SPT_HIP(hipMemsetAsync(c->stats + 14, 0xFF, sizeof(unsigned long long), stream));
 #endif
-  c->nee_by_identity = kv == KV_CONST_NEE_CAM || kv == KV_UPBOX_NEE_CAM ||
+  c->nee_by_identity = kv == KV_CONST_NEE_CAM || kv == KV_UPBOX_NEE_CAM || kv == KV_UPLIGHT_NEE ||
+                       kv == KV_UPLIGHT_NEE_CAM ||
                        kv == KV_CONST_NEE || kv == KV_SPHDIFF_NEE || kv == KV_CONST_NEE_REF ||
                        kv == KV_SPHDIFF_NEE_REF || kv == KV_CORNELL_NEE || kv == KV_RECTDIFF_NEE ||
                        kv == KV_UPBOX_NEE;
