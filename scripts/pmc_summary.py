@@ -23,9 +23,16 @@ for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True
         if kname in r["Kernel_Name"]:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
 avg = {k: sum(v) / len(v) for k, v in vals.items()}
+# The kernel build these counters belong to (bench.py checks it before using them): the hash the
+# library was built with (embedded by make, spt_build_sources_sha16; SPT_LIB selects an A/B build),
+# which must equal the tree's -- a summary of counters from other sources is refused.
+spt = importlib.import_module("small-pathtracer_amd")
+built, tree = spt.build_sources_sha16(), spt.kernel_sources_sha16()
+if built != tree:
+    sys.exit(f"pmc_summary: {spt.LIB_PATH} was built from kernel sources {built}, the tree has {tree}; "
+             f"rebuild it (or summarise on the tree it was built from)")
 out = {"kernel": kname, "dispatches": {k: len(v) for k, v in vals.items()}, "counters": avg,
-       # the kernel build these counters belong to (bench.py checks it before using them)
-       "kernel_sources_sha16": importlib.import_module("small-pathtracer_amd").kernel_sources_sha16()}
+       "kernel_sources_sha16": built}
 if durs:
     out["avg_duration_ms"] = 1e3 * sum(durs) / len(durs)
 d = out.get("avg_duration_ms")

@@ -65,3 +65,17 @@ def test_hung_rank_is_ended_at_the_launch_timeout():
     assert r.returncode == 124, (r.returncode, r.stderr)
     assert time.monotonic() - t0 < 60
     assert "ending them (status 124)" in r.stderr
+
+
+def test_eight_spawned_ranks_forward_exactly_one_json_line():
+    """The driver's 8-GPU form without a launcher (`bench.py --gpus 8`): eight probe ranks start with
+    RANK 0..7 and one MASTER_PORT, and the parent's stdout holds exactly one JSON line (rank 0's);
+    the other seven ranks' lines go to stderr."""
+    r = run(["--gpus", "8", "--probe-env"])
+    assert r.returncode == 0, r.stderr
+    out = lines(r.stdout)
+    assert len(out) == 1 and out[0]["RANK"] == "0" and out[0]["WORLD_SIZE"] == "8"
+    assert [x for x in r.stdout.splitlines() if x.strip()] == [r.stdout.strip()]
+    got = sorted(out + lines(r.stderr), key=lambda d: int(d["RANK"]))
+    assert [d["RANK"] for d in got] == [str(i) for i in range(8)]
+    assert len({d["MASTER_PORT"] for d in got}) == 1
