@@ -2,8 +2,12 @@
 # Measurement session on the GPU box (in-tree build): GPU tests, the C3 rocprofv3 session (kernel
 # trace + separate PMC passes, scripts/profile.sh), instruction-class PMC passes, and the bench lines
 # of every config (C2-C5, with their CPU baselines). Outputs are tagged with TAG (default r04).
-#   PARTS="pytest smoke rehearsal profile classes dropin bench" selects parts; each GPU step has its own time limit and the
-#   script stops at the first failure.
+#   PARTS="record pytest smoke rehearsal profile classes waves dropin levels bench" selects parts;
+#   each GPU step has its own time limit and the script stops at the first failure.
+#   record: scripts/gpu_record.py TAG (pytest -m gpu + smoke, stamped; SPT_GIT_HEAD from the caller)
+#   waves:  per-wave dumps of C2 and C3 with the SPT_DIAG=2 build (build/ab/diag2.so, made by
+#           scripts/build_variants.sh diag2:"-DSPT_DIAG=2" beforehand) -> gpurun_out/TAG_waves_*.json
+#   levels: scripts/levels.sh (kernel levels at C3 / C2)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -11,6 +15,10 @@ mkdir -p gpurun_out
 PARTS=${PARTS:-"pytest profile classes bench"}
 TAG=${TAG:-r04}
 has() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
+if has record; then
+  timeout -k 10 900 python -u scripts/gpu_record.py $TAG > gpurun_out/${TAG}_record.log 2>&1
+  rc=$?; echo "gpu_record exit $rc"; tail -2 gpurun_out/${TAG}_record.log; [ $rc -eq 0 ] || exit $rc
+fi
 if has pytest; then
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_gpu.log 2>&1
@@ -46,6 +54,16 @@ if has classes; then
     done
     python3 scripts/pmc_summary.py gpurun_out/cls_$cfg > gpurun_out/cls_$cfg/summary.json
   done
+fi
+if has waves; then
+  for cfg in c2 c3; do
+    SPT_LIB=build/ab/diag2.so timeout -k 10 180 python tools/wave_dump.py $cfg gpurun_out/${TAG}_waves_$cfg.bin \
+      > gpurun_out/${TAG}_waves_$cfg.json 2> gpurun_out/${TAG}_waves_$cfg.err
+    rc=$?; echo "waves $cfg exit $rc"; [ $rc -eq 0 ] || exit $rc
+  done
+fi
+if has levels; then
+  TAG=$TAG bash scripts/levels.sh || exit $?
 fi
 if has dropin; then  # the drop-in program end to end (tools/dropin_e2e.py) and its kernels under rocprofv3
   timeout -k 10 600 python tools/dropin_e2e.py --ref-spp 8 --out gpurun_out/${TAG}_dropin.json \

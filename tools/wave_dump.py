@@ -57,6 +57,12 @@ def main():
     res = {"config": cfg, "kernel_ms": st["kernel_ms"], "waves": int(len(a)), "span_us": span / 100.0,
            "mean_resident_frac": float((t1 - t0).sum() / (len(a) * span)),
            "iters_total": int(iters.sum()),
+           # a resident wave's time per loop iteration, and the span if every wave slot stayed
+           # resident to the end at that rate (the residency-limited bound of a perfectly balanced tail)
+           "wave_ns_per_iter": float((t1 - t0).sum() * 10.0 / iters.sum()),
+           "balanced_span_us": float((t1 - t0).sum() / len(a) / 100.0),
+           "end_quantiles_frac_of_span": {str(q): float(np.quantile((t1 - start) / span, q))
+                                          for q in (0.01, 0.1, 0.5, 0.9, 0.99)},
            "by_age_rank": {}}
     for k in range(int(rank.max()) + 1):
         m = rank == k
