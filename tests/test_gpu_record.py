@@ -16,7 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _newest_record():
     recs = glob.glob(os.path.join(ROOT, "profiles", "r*_gpu_tests.json"))
     assert recs, "no profiles/r*_gpu_tests.json GPU test record committed"
-    key = lambda p: (int(re.match(r"r(\d+)", os.path.basename(p)).group(1)), os.path.getmtime(p))  # noqa: E731
+    # newest by round, then by the record's own UTC stamp (file mtimes do not survive a checkout)
+    key = lambda p: (int(re.match(r"r(\d+)", os.path.basename(p)).group(1)),  # noqa: E731
+                     json.load(open(p)).get("utc", ""))
     return max(recs, key=key)
 
 
