@@ -676,3 +676,18 @@ def test_edited_light_cosine_bit_exact(spt, oracle, edit):
     gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
     _assert_exact(gpu, cpu)
     assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+
+
+def test_material_edits_keep_the_literal_kernel(spt, oracle):
+    """Only geometry is literal in the HEAD kernels: a brighter light (:294 emission 15) and a blue
+    left wall (:290) run the literal HEAD NEE kernel (its early resolve: shadow_proven > 0), bit-exact
+    with the oracle."""
+    prims = [spt.spt_prim.from_buffer_copy(p) for p in spt.cornell_scene()]
+    for i in range(3):
+        prims[6].e[i] = 15.0
+    prims[2].c[0], prims[2].c[1], prims[2].c[2] = 0.25, 0.25, 0.75
+    p = spt.default_params(width=64, height=48, spp=16, seed=21)
+    gpu, gst, cpu, cst = _render_both(spt, oracle, prims, p)
+    _assert_exact(gpu, cpu)
+    assert {k: gst[k] for k in spt.STAT_KEYS} == cst
+    assert gst["shadow_proven"] > 0
