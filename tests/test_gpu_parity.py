@@ -131,18 +131,19 @@ def test_every_kernel_specialisation_bit_exact(spt, oracle, kernel, est, q, fl):
 TILTED = dict(lookfrom=(40, 55, 160), lookat=(55, 35, 10), vup=(0.1, 1, 0))
 
 
-@pytest.mark.parametrize("scene", ["head", "edited"])
+@pytest.mark.parametrize("scene", ["head", "edited", "movebox"])
 @pytest.mark.parametrize("flags", [0, 4, 2 << 8])
 @pytest.mark.parametrize("est,q", [("nee", 1.0), ("cos", 0.0)])
 def test_tilted_camera_bit_exact(spt, oracle, est, q, flags, scene):
     """A camera whose horizontal/vertical vectors are not axis-aligned (Camera :262-275 with another
     lookat and vup). Round 6: the literal kernels' any-camera forms (Cfg CAMAX 2: KV_CONST_*_CAM on
-    the HEAD scene, KV_UPBOX_*_CAM on an edited one with the HEAD room) keep the early shadow-ray
-    resolve; flags 4 (the reference's leaks) and the cornell cap (2 << 8) take the run-time camera
+    the HEAD scene, KV_UPBOX_*_CAM with a box moved, KV_UPLIGHT_*_CAM with the light edited) keep
+    the early shadow-ray resolve; flags 4 (the reference's leaks) and the cornell cap (2 << 8) take the run-time camera
     kernels. Same contract, same bits, and (NEE, auto) shadow rays resolved without a trace."""
     import test_oracle as to
 
     prims = (spt.cornell_scene() if scene == "head" else
+             spt.move_short_box(spt.cornell_scene(), 1.0) if scene == "movebox" else
              to.edited_scene(spt, **to.EDITS_LR[1][0]))
     p = spt.default_params(width=48, height=36, spp=8, seed=17, nee_prob=q, flags=flags)
     cam = spt.Camera(aspect=48 / 36, **TILTED)
