@@ -402,6 +402,10 @@ def main() -> None:
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
                     help="--gpus N > 1 without a launcher: seconds the spawned ranks may run in all "
                          "before they are ended (exit status 124)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="profiling sessions only: skip everything after the timed region that launches "
+                         "the render kernel again (the reference-leaks leg, the quality renders), so a "
+                         "rocprofv3 summary of the run averages the warm-up and timed dispatches only")
     ap.add_argument("--probe-env", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -778,7 +782,7 @@ def main() -> None:
             spt.write_ppm(args.save_ppm, img)
         writer = image_writer(spt, full, w, h, with_cpu=not args.no_cpu_baseline)
         qual = None
-        if (args.config in QUALITY_FIXTURES and world == 1 and not edited
+        if (args.config in QUALITY_FIXTURES and world == 1 and not edited and not args.no_extras
                 and os.path.exists(QUALITY_FIXTURES[args.config][0])):
             # 15 more seeds of the same render (after the timed region): the matched-budget RMSE
             extra = [spt.render(prims, cam, spt.default_params(
@@ -794,7 +798,7 @@ def main() -> None:
         # bench image: K steps through the same pipeline (value_reference_leaks) and 3 isolated
         # launches (kernel_ms_reference_leaks), VERDICT r05 item 4
         leak = None
-        if world == 1 and cfg["scene"] == "cornell":
+        if world == 1 and cfg["scene"] == "cornell" and not args.no_extras:
             if args.reference_leaks:
                 leak = {"rule": "off: leaked paths go on from the miss vertex as the reference's "
                                 "(:371-377, SPT_FLAG_REFERENCE_LEAKS)"}

@@ -8,7 +8,9 @@ TAG=${1:-run}; shift || true
 # one frame in flight: every render dispatch runs alone, so the trace's average duration is the
 # isolated kernel time the bench line's roofline.kernel_ms reports (two overlapping frames stretch
 # each other's dispatch spans)
-ARGS=${*:---steps 6 --warmup 2 --no-cpu-baseline --frames-in-flight 1}
+# --no-extras: no render launches after the timed region (reference-leaks leg, quality renders), so
+# the --stats summary's average is the warm-up and timed dispatches of the one kernel
+ARGS=${*:---steps 20 --warmup 3 --no-cpu-baseline --frames-in-flight 1 --no-extras}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 run() {  # name, rocprof args...

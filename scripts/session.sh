@@ -38,7 +38,7 @@ if has classes; then
   # CLS: configurations (tag[:chunk]); c2:32 = C2 at 32-sample units (the C2 tail study)
   for spec in ${CLS:-c3 c5}; do
     cfg=${spec%%:*}; tag=$cfg
-    args="--steps 2 --warmup 1 --no-cpu-baseline --config $cfg"
+    args="--steps 2 --warmup 1 --no-cpu-baseline --no-extras --config $cfg"
     [ $cfg = c5 ] && args="$args --spp 256"
     case $spec in *:*) args="$args --chunk ${spec#*:}"; tag=${cfg}_u${spec#*:};; esac
     mkdir -p gpurun_out/cls_$tag; cfg=$tag
