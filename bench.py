@@ -915,6 +915,10 @@ def main() -> None:
             "ranks": per_rank,
             "cpu_baseline": cpu,
             "image_writer": writer,
+            # the kernel build this line measured (the GPU test record profiles/rNN_gpu_tests.json
+            # carries the same hash)
+            "build": {"kernel_sources_sha16": spt.kernel_sources_sha16(),
+                      "libspt_build_sources_sha16": spt.build_sources_sha16()},
         }
         print(json.dumps(out), flush=True)
     for r_ in rens:
