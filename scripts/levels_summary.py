@@ -41,6 +41,7 @@ out["_session"] = (f"scripts/levels.sh (TAG={tag}): bench.py --steps 5 --warmup 
                    f"per level, one box; kernel_ms_isolated = 3 launches one at a time after the timed "
                    f"region")
 out["_kernel_sources_sha16"] = spt.kernel_sources_sha16()
+out["_libspt_build_sources_sha16"] = spt.build_sources_sha16()
 json.dump(out, open(os.path.join(ROOT, "profiles", f"{tag}_kernel_levels_c3.json"), "w"), indent=1)
 for k, v in out.items():
     if not k.startswith("_"):
