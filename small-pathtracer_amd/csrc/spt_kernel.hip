@@ -81,8 +81,9 @@ constexpr uint32_t kGrabMin = SPT_GRAB_MIN;  // guided grabs never take fewer (b
 // mille of the units are handed out. The SIMD issues oldest-first, so these waves get the fewest
 // slots (C3: the two youngest of a CU's 8 blocks do ~4 % of the work) and the units they hold end
 // the launch. Round 5 A/B (profiles/r05_young_cut_ab.json): C3 isolated kernel -1.3 to -1.6 %,
-// C4 -0.8 %, values flat; applied to the literal HEAD NEE kernels and the boxes-only-uploaded NEE
-// kernel (KV_UPBOX_NEE, edited scenes: -4 %) only (the others lost). It assumes the dispatcher hands
+// C4 -0.8 %, values flat; applied to the literal HEAD NEE kernels (and their any-camera forms) and
+// the room-literal edited-scene NEE kernels (KV_UPBOX_NEE: -4 %; KV_UPLIGHT_NEE, round 6) only (the
+// others lost). It assumes the dispatcher hands
 // each CU its blocks in blockIdx order, so blockIdx >= SPT_YOUNG_RANK x n_cu are the blocks a CU
 // received last; that holds only with every CU full at 8 blocks, so the host applies it at bpc == 8.
 #ifndef SPT_YOUNG_CUT
@@ -547,8 +548,9 @@ __device__ __forceinline__ RectHit rect_eval(GP g, const Ray6& r) {
   const bool ia = fabsf(a) <= g->ha, ib = fabsf(b) <= g->hb;
   return RectHit{tt, (bool)((int)ia & (int)ib), a};
 }
-// The uploaded light of the boxes-only-uploaded kernels (a single XZ test at the HEAD light's grouped
-// position, from LDS): rect_cand's arithmetic for a single, with the position literal.
+// The uploaded light of the room-literal UPLIGHT kernels (a single XZ test at the HEAD light's grouped
+// position, read from the uploaded scene through scalar loads): rect_cand's arithmetic for a single,
+// with the position literal.
 template <class GT>
 __device__ __forceinline__ void light_cand(const GT& g, const Ray6& r, uint32_t& tmin) {
   const float t0 = plane_t(g.k0 - r.oa, r.ia);
