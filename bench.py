@@ -523,16 +523,32 @@ def main() -> None:
     # torch.distributed.gather into rank 0's pre-allocated slots, de-interleaved on the device
     # (distributed.gather_rows, the path the gloo tests cover)
     slots = [torch.zeros_like(shard) for _ in range(world)] if use_torch_gather and rank == 0 else None
+    comm_error = ""
     if world > 1 and backend == "nccl" and not use_torch_gather:
         # the framebuffer gather of SURVEY §8e in the library (spt_comm: C++ over RCCL, grouped
         # ncclSend/ncclRecv to rank 0 + the de-interleave kernel); torch.distributed only carries
         # the RCCL unique id from rank 0 to the others
         uid = [spt.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        comm = spt.Comm(uid[0], world, rank, local)
-        comm.reserve(params)
+        try:  # (a rank whose communicator fails to come up takes the torch fallback below)
+            comm = spt.Comm(uid[0], world, rank, local)
+            comm.reserve(params)
+        except Exception as e:  # noqa: BLE001
+            comm, comm_error = None, f"{type(e).__name__}: {e}"
+            log(f"bench.py: rank {rank}: spt_comm set-up failed ({comm_error})")
+        up = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(up, op=dist.ReduceOp.MIN)
+        if int(up.item()) == 0:
+            if comm is not None:
+                comm.close()
+            comm = None
+            use_torch_gather = True
+            slots = [torch.zeros_like(shard) for _ in range(world)] if rank == 0 else None
     gather_mode = "spt (RCCL send/recv)" if comm is not None else (
         "torch (dist.gather)" if use_torch_gather else ("host (gloo)" if world > 1 else "none"))
+    if world > 1 and backend == "nccl" and args.gather == "spt" and comm is None:
+        gather_mode = ("torch (dist.gather; spt_comm set-up failed on a rank"
+                       + (f": {comm_error})" if comm_error else ")"))
     if comm is not None:
         # The library gather has not run on >1 GPU before the driver's scaling run: check it on a
         # known pattern (every rank's rows, exact in fp32) before anything is timed, and fall back
