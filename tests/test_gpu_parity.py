@@ -599,19 +599,28 @@ def test_edited_cornell_scene_bit_exact(spt, oracle, kernel, nee):
     assert not np.array_equal(base, gpu)  # the edit is visible
 
 
+@pytest.mark.parametrize("scene", ["head", "light_tilted"])
 @pytest.mark.parametrize("flags", [0, 4])
-def test_full_size_scheduling_never_changes_results(spt, flags):
+def test_full_size_scheduling_never_changes_results(spt, flags, scene):
     """At C3's full size the launch is long, so the young-block cut (SPT_YOUNG_CUT)
     is active: the two youngest blocks of each CU stop taking work after 30 % of the units. Units of
     another size hand different samples to different lanes and blocks, and the image and every
     path statistic must stay identical (integer accumulation, counter RNG). flags 4: the reference's
-    leaks (SPT_FLAG_REFERENCE_LEAKS, the other kernel the cut applies to)."""
+    leaks (SPT_FLAG_REFERENCE_LEAKS, the other kernel the cut applies to). light_tilted: an edited
+    light seen through a tilted camera (KV_UPLIGHT_NEE_CAM, the cut applies; with flags 4 the
+    run-time Cornell kernel)."""
+    import test_oracle as to
+
     w, h, spp = 1024, 768, 512
-    cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    if scene == "head":
+        prims, cam = spt.cornell_scene(), spt.Camera(aspect=float(np.float32(w) / np.float32(h)))
+    else:
+        prims = to.edited_scene(spt, light=dict(y=81.4))
+        cam = spt.Camera(aspect=float(np.float32(w) / np.float32(h)), **TILTED)
     runs = []
     for chunk in (0, 64):
         p = spt.default_params(width=w, height=h, spp=spp, seed=7, flags=flags, chunk=chunk)
-        runs.append(spt.render(spt.cornell_scene(), cam, p, return_stats=True))
+        runs.append(spt.render(prims, cam, p, return_stats=True))
     (a, sa), (b, sb) = runs
     assert np.array_equal(a, b)
     assert {k: sa[k] for k in spt.STAT_KEYS} == {k: sb[k] for k in spt.STAT_KEYS}
