@@ -203,6 +203,17 @@ def proof_counts() -> tuple:
     return int(out[0]), int(out[1])
 
 
+def shadow_census() -> list:
+    """Test hook (tools/shadow_census.py): the light-accepted shadow rays the HEAD early resolve
+    left to a trace since the last call, by outcome and failing clause (spt_oracle_shadow_census,
+    proof mode 1); resets the counts."""
+    out = (ctypes.c_uint64 * 16)()
+    L = lib()
+    L.spt_oracle_shadow_census.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    L.spt_oracle_shadow_census(out)
+    return [int(v) for v in out]
+
+
 def set_pairs(on: bool) -> None:
     """Test hook: parallel-pair rect tests on (the contract) or off (every rect on its own)."""
     lib().spt_oracle_set_pairs(1 if on else 0)

@@ -567,3 +567,26 @@ def test_early_nee_resolve_proof_holds_edited_light_and_room(oracle, spt, edit):
         assert claims > 0.3 * st["nee_light_hits"], (claims, st["nee_light_hits"])
     else:
         assert claims == 0 and st["nee_light_hits"] > 0, (claims, st["nee_light_hits"])
+
+
+def test_shadow_census_accounts_for_every_traced_shadow_ray(oracle):
+    """The slot model's census (tools/shadow_census.py): every light-accepted shadow
+    ray the HEAD early resolve does not prove is counted once, as reached or blocked, and the
+    sub-classes never exceed their class."""
+    w, h, spp = 64, 48, 16
+    p = oracle.default_params(width=w, height=h, spp=spp, seed=23)
+    oracle.shadow_census()  # reset
+    oracle.proof_check(True)
+    try:
+        _, st = oracle.counter_render(oracle.scene_cornell(), oracle.camera(w / h), p)
+        claims, bad = oracle.proof_counts()
+    finally:
+        oracle.proof_check(False)
+    c = oracle.shadow_census()
+    assert bad == 0
+    assert c[0] + c[1] == st["shadow_traced"] - claims, (c[:2], st["shadow_traced"], claims)
+    assert c[0] == st["nee_light_hits"] - claims  # every traced ray that reached the light
+    assert c[3] + c[4] <= c[1] and c[5] <= c[3]  # blocked: vertex outside the room; self-hits
+    # reached: by failing box clause; a vertex outside the room never reaches the light (its own
+    # wall's slab candidate is the entry at a tiny t)
+    assert c[6] + c[7] + c[8] <= c[0] and c[2] == 0

@@ -3,7 +3,6 @@
 shadow rays the HEAD NEE kernel still traces (early_nee_proven fails), by outcome and by the
 predicate's failing clause, from the oracle (the same contract and Philox streams as the kernel).
 Writes profiles/r06_shadow_census.json.  usage: python tools/shadow_census.py [W H SPP]"""
-import ctypes
 import importlib
 import json
 import os
@@ -14,8 +13,6 @@ sys.path.insert(0, ROOT)
 from oracle import oracle  # noqa: E402  (test infrastructure: the checker, not the product)
 
 w, h, spp = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 192, 32)
-L = oracle.lib()
-L.spt_oracle_shadow_census.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
 p = oracle.default_params(width=w, height=h, spp=spp, seed=3)
 oracle.proof_check(True)
 try:
@@ -23,8 +20,7 @@ try:
     claims, bad = oracle.proof_counts()
 finally:
     oracle.proof_check(False)
-c = (ctypes.c_uint64 * 16)()
-L.spt_oracle_shadow_census(c)
+c = oracle.shadow_census()
 n = w * h * spp
 per = lambda v: round(v / n, 4)  # noqa: E731
 traced = c[0] + c[1]
